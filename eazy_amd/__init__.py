@@ -1,0 +1,504 @@
+"""eazy_amd — MI355X-native eazy codec: Python binding of include/eazy.h.
+
+The shipped path is libeazy_amd.so (gfx950 HIP kernels behind a C-ABI).
+This module is a thin ctypes layer over it:
+
+* ``Writer`` / ``Reader`` mirror the reference's streaming types
+  (writer.go:17-46, reader.go:17-40) with the same field names, flush policy
+  and error values; their compression / decompression runs on the GPU.
+* ``compress_batch`` / ``pack`` / ``decompress_batch`` drive the batched,
+  device-resident kernels (K1/K3/K2) on torch CUDA tensors.
+* ``Encoder`` / ``Decoder`` expose the token codec (writer.go:537-621,
+  reader.go:346-514).
+
+There is no CPU fallback: importing works without a GPU (for the build and
+symbol checks), but every compute call raises ``DeviceError`` when the HIP
+runtime has no MI355X.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libeazy_amd.so")
+
+# ---- constants (writer.go:49-122) ----
+B, KiB, MiB, GiB = 1, 1 << 10, 1 << 20, 1 << 30
+Literal, Copy, Meta, Padding = 0x00, 0x80, 0x80, 0x00
+TagMask, TagLenMask = 0x80, 0x7F
+Len1, Len2, Len4, LenAlt = 124, 125, 126, 127
+Off1, Off2, Off4, OffAlt = 252, 253, 254, 255
+OffLong = OffAlt
+MetaMagic, MetaVer, MetaReset, MetaBreak = 0x00, 0x08, 0x10, 0x18
+MetaTagMask, MetaLenMask, MetaLenWide, MetaLen0 = 0xF8, 0x07, 6, 7
+Magic = b"\x80\x02eazy"
+Version = 0
+
+# ---- status codes (include/eazy.h) ----
+OK, EOF, ESHORTBUF, EUNEXPECTEDEOF, EOVERFLOW, EBADMAGIC, ENOMAGIC = 0, 1, 2, 3, 4, 5, 6
+EBLOCKLIMIT, EUNSUPMETA, EUNSUPVER, EBREAK, EMISSEDMETA, EINVAL = 7, 8, 9, 10, 11, 12
+ESINK, ENOSPC, EDEVICE, ESTUCK = 13, 14, 15, 16
+F_NO_MAGIC = 0x1
+
+
+class EazyError(Exception):
+    code = -1
+
+    def __init__(self, code: int, detail: int = 0):
+        self.code = code
+        self.detail = detail
+        super().__init__(f"{_strerror(code)}" + (f": {detail:#x}" if detail else ""))
+
+
+class DeviceError(EazyError):
+    """No usable MI355X (or a HIP runtime error) — there is no CPU fallback."""
+
+
+class Panic(EazyError):
+    """Where the reference panics (bad sizes, too big length/offset, bad meta)."""
+
+
+def _strerror(code: int) -> str:
+    try:
+        return _lib().ez_strerror(code).decode()
+    except OSError:
+        return f"code {code}"
+
+
+_L = None
+
+
+def _lib():
+    global _L
+    if _L is not None:
+        return _L
+    if not os.path.exists(LIB_PATH):
+        raise OSError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C eazy_amd)")
+    L = C.CDLL(LIB_PATH)
+    sz, i64, u8p, vp = C.c_size_t, C.c_int64, C.POINTER(C.c_uint8), C.c_void_p
+    L.ez_strerror.restype = C.c_char_p
+    L.ez_strerror.argtypes = [C.c_int]
+    L.ez_compress_bound.restype = sz
+    L.ez_compress_bound.argtypes = [sz]
+    for f in ("ez_encode_tag", "ez_encode_offset", "ez_encode_meta"):
+        getattr(L, f).argtypes = [u8p, sz, C.POINTER(sz), i64, i64]
+    L.ez_encode_tag.argtypes = [u8p, sz, C.POINTER(sz), C.c_int, i64]
+    L.ez_decode_tag.argtypes = [C.c_char_p, sz, sz, C.POINTER(C.c_int), C.POINTER(i64), C.POINTER(sz)]
+    L.ez_decode_offset.argtypes = [C.c_char_p, sz, sz, i64, C.POINTER(i64), C.POINTER(sz)]
+    L.ez_decode_meta.argtypes = [C.c_char_p, sz, sz, C.POINTER(i64), C.POINTER(i64), C.POINTER(sz)]
+    L.ez_writer_new.argtypes = [i64, i64, C.c_int, C.POINTER(vp)]
+    L.ez_writer_free.argtypes = [vp]
+    L.ez_writer_set_append_magic.argtypes = [vp, C.c_int]
+    L.ez_writer_set_version.argtypes = [vp, C.c_int]
+    L.ez_writer_write.argtypes = [vp, C.c_char_p, sz, vp, sz, C.POINTER(sz)]
+    L.ez_writer_header.argtypes = [vp, vp, sz, C.POINTER(sz)]
+    L.ez_writer_break.argtypes = [vp, vp, sz, C.POINTER(sz)]
+    L.ez_writer_reset.argtypes = [vp]
+    L.ez_writer_reset_size.argtypes = [vp, i64, i64]
+    L.ez_writer_is_reset.argtypes = [vp]
+    L.ez_reader_new.argtypes = [C.c_int, C.POINTER(vp)]
+    L.ez_reader_free.argtypes = [vp]
+    L.ez_reader_configure.argtypes = [vp, i64, C.c_int, C.c_int]
+    L.ez_reader_reset.argtypes = [vp]
+    L.ez_reader_pending.argtypes = [vp]
+    L.ez_reader_read.argtypes = [vp, vp, sz, sz, i64, vp, sz, C.POINTER(sz), C.POINTER(sz), C.POINTER(i64)]
+    L.ez_compress_batch.argtypes = [i64, i64, C.c_int, vp, vp]
+    L.ez_pack_workspace.restype = sz
+    L.ez_pack_workspace.argtypes = [C.c_uint64]
+    L.ez_pack_batch.argtypes = [vp, vp, vp, C.c_uint64, vp, vp, vp, vp]
+    L.ez_decompress_batch.argtypes = [i64, vp, vp]
+    _L = L
+    return L
+
+
+def exported_symbols() -> list[str]:
+    """Names declared in include/eazy.h that the library must export."""
+    import re
+
+    hdr = open(os.path.join(_HERE, "..", "include", "eazy.h")).read()
+    return sorted(set(re.findall(r"\b(ez_[a-z_0-9]+)\s*\(", hdr)))
+
+
+def device_count() -> int:
+    return _lib().ez_device_count()
+
+
+def _check(code: int, detail: int = 0) -> None:
+    if code == OK:
+        return
+    if code == EDEVICE:
+        raise DeviceError(code)
+    if code == EINVAL:
+        raise Panic(code)
+    raise EazyError(code, detail)
+
+
+def compress_bound(n: int) -> int:
+    return _lib().ez_compress_bound(n)
+
+
+# ---------------------------------------------------------------- token codec
+
+
+class Encoder:
+    """Low-level encoder (writer.go:10-15, 537-621)."""
+
+    def __init__(self, ver: int = 0):
+        self.Ver = ver
+
+    @staticmethod
+    def _enc(fn, *args) -> bytes:
+        buf = (C.c_uint8 * 32)()
+        n = C.c_size_t(0)
+        _check(getattr(_lib(), fn)(buf, 32, C.byref(n), *args))
+        return bytes(buf[: n.value])
+
+    def tag(self, b: bytes, tag: int, l: int) -> bytes:
+        return bytes(b) + self._enc("ez_encode_tag", tag, l)
+
+    def offset(self, b: bytes, off: int, l: int) -> bytes:
+        return bytes(b) + self._enc("ez_encode_offset", off, l)
+
+    def meta(self, b: bytes, meta: int, l: int) -> bytes:
+        return bytes(b) + self._enc("ez_encode_meta", meta, l)
+
+
+class Decoder:
+    """Low-level decoder (reader.go:10-15, 346-514): returns Go's results, err as code."""
+
+    def __init__(self, ver: int = 0):
+        self.Ver = ver
+
+    def tag(self, b: bytes, st: int):
+        t, l, i = C.c_int(), C.c_int64(), C.c_size_t()
+        e = _lib().ez_decode_tag(bytes(b), len(b), st, C.byref(t), C.byref(l), C.byref(i))
+        return t.value, l.value, i.value, e
+
+    def offset(self, b: bytes, st: int, l: int):
+        off, i = C.c_int64(), C.c_size_t()
+        e = _lib().ez_decode_offset(bytes(b), len(b), st, l, C.byref(off), C.byref(i))
+        return off.value, i.value, e
+
+    def meta(self, b: bytes, st: int):
+        m, l, i = C.c_int64(), C.c_int64(), C.c_size_t()
+        e = _lib().ez_decode_meta(bytes(b), len(b), st, C.byref(m), C.byref(l), C.byref(i))
+        return m.value, l.value, i.value, e
+
+
+# ---------------------------------------------------------------- Writer
+
+
+class Writer:
+    """eazy.Writer (writer.go:17-46): NewWriter(wr, block, htable).
+
+    ``wr`` is an io.Writer-like object whose ``write(bytes)`` returns the
+    number of bytes taken (or raises).  One Write -> one wr.write (with
+    FlushThreshold 0), header on the first Write, a failed or short sink
+    write resets the stream (writer.go:387-401).
+    """
+
+    def __init__(self, wr, block: int, htable: int, device: int = 0):
+        h = C.c_void_p()
+        _check(_lib().ez_writer_new(block, htable, device, C.byref(h)))
+        self._h = h
+        self.Writer = wr
+        self._append_magic = True
+        self.FlushThreshold = 0
+        self._ver = 0
+        self._b = bytearray()
+        self._written = 0
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib().ez_writer_free(self._h)
+            self._h = None
+
+    @property
+    def AppendMagic(self) -> bool:
+        return self._append_magic
+
+    @AppendMagic.setter
+    def AppendMagic(self, on: bool) -> None:
+        self._append_magic = bool(on)
+        _lib().ez_writer_set_append_magic(self._h, int(bool(on)))
+
+    @property
+    def Ver(self) -> int:  # w.e.Ver
+        return self._ver
+
+    @Ver.setter
+    def Ver(self, v: int) -> None:
+        self._ver = int(v)
+        _lib().ez_writer_set_version(self._h, int(v))
+
+    def _call(self, fn, *args, cap: int) -> bytes:
+        buf = (C.c_uint8 * max(cap, 1))()
+        n = C.c_size_t()
+        _check(fn(self._h, *args, buf, cap, C.byref(n)))
+        return bytes(buf[: n.value])
+
+    def Write(self, p: bytes) -> int:  # writer.go:206-337
+        p = bytes(p)
+        self._b += self._call(_lib().ez_writer_write, p, len(p), cap=compress_bound(len(p)))
+        self._write()
+        return len(p)
+
+    def WriteHeader(self) -> None:  # writer.go:342-350
+        if not _lib().ez_writer_is_reset(self._h):
+            return
+        self._b += self._call(_lib().ez_writer_header, cap=32)
+        self._write()
+
+    def WriteBreak(self) -> None:  # writer.go:358-366
+        self._b += self._call(_lib().ez_writer_break, cap=32)
+        self._write()
+
+    def Flush(self) -> None:  # writer.go:371-377
+        if self._b:
+            self._flush()
+
+    def Reset(self, wr) -> None:  # writer.go:149-152
+        self.Writer = wr
+        self._reset()
+
+    def ResetSize(self, wr, block: int, htable: int) -> None:  # writer.go:155-159
+        self.Writer = wr
+        _check(_lib().ez_writer_reset_size(self._h, block, htable))
+        self._b = bytearray()
+        self._written = 0
+
+    def _reset(self) -> None:  # writer.go:187-200
+        _check(_lib().ez_writer_reset(self._h))
+        self._b = bytearray()
+        self._written = 0
+
+    def _write(self) -> None:  # writer.go:379-385
+        if self.FlushThreshold < 0 or len(self._b) < self.FlushThreshold:
+            return
+        self._flush()
+
+    def _flush(self) -> None:  # writer.go:387-401
+        try:
+            n = self.Writer.write(bytes(self._b))
+            err = None
+        except Exception as e:  # noqa: BLE001 - any sink error resets the stream
+            n, err = getattr(e, "n", 0), e
+        n = len(self._b) if n is None else n
+        self._written += n
+        if err is not None or n != len(self._b):
+            self._reset()
+        if err is not None:
+            raise err
+        self._b = bytearray()
+
+
+def NewWriter(wr, block: int, htable: int, device: int = 0) -> Writer:
+    return Writer(wr, block, htable, device)
+
+
+# ---------------------------------------------------------------- Reader
+
+
+class Reader:
+    """eazy.Reader (reader.go:17-40).  NewReader(r) / NewReaderBytes(b).
+
+    ``Read(n)`` returns ``(data, err)`` with err one of the status codes
+    (OK, EOF, EBREAK, ...), exactly the (n, err) pair of Go's Read.
+    ``r`` is either an object with ``read_go(k) -> (bytes, err_code)`` (Go
+    io.Reader semantics, e.g. data together with EOF) or a Python file-like
+    whose ``read(k)`` returns b"" at EOF.
+    """
+
+    def __init__(self, r=None, b: bytes | None = None, device: int = 0):
+        h = C.c_void_p()
+        _check(_lib().ez_reader_new(device, C.byref(h)))
+        self._h = h
+        self.Reader = r
+        self._b = bytearray(b or b"")
+        self._i = 0
+        self._boff = 0
+        self.BlockSizeLimit = 16 * MiB if r is not None else 0
+        self.BufferSize = 64 * 1024 if r is not None else 0
+        self.RequireMagic = False
+        self.SkipUnsupportedMeta = False
+        self.detail = 0
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _lib().ez_reader_free(self._h)
+            self._h = None
+
+    def Reset(self, rd) -> None:  # reader.go:96-99
+        self.ResetBytes(b"")
+        self.Reader = rd
+
+    def ResetBytes(self, b: bytes) -> None:  # reader.go:102-113
+        self.Reader = None
+        self._b = bytearray(b)
+        self._i = 0
+        self._boff = 0
+        _lib().ez_reader_reset(self._h)
+
+    def Read(self, n: int):  # reader.go:116-141
+        L = _lib()
+        L.ez_reader_configure(self._h, self.BlockSizeLimit, int(self.RequireMagic), int(self.SkipUnsupportedMeta))
+        p = (C.c_uint8 * max(n, 1))()
+        got, err = 0, OK
+        while got < n and err == OK:
+            bb = (C.c_uint8 * max(len(self._b), 1)).from_buffer_copy(bytes(self._b) or b"\0")
+            m, i, det = C.c_size_t(), C.c_size_t(), C.c_int64()
+            err = L.ez_reader_read(self._h, bb, len(self._b), self._i, self._boff,
+                                   C.byref(p, got), n - got, C.byref(m), C.byref(i), C.byref(det))
+            if err == EDEVICE:
+                raise DeviceError(err)
+            got += m.value
+            self._i = i.value
+            self.detail = det.value
+            if got == n:
+                break
+            if err != ESHORTBUF:
+                continue
+            err = self._more()
+            if err == EOF and (L.ez_reader_pending(self._h) or self._i < len(self._b)):
+                err = EUNEXPECTEDEOF
+        return bytes(p[:got]), err
+
+    def _more(self) -> int:  # reader.go:516-543
+        if self.Reader is None:
+            return EOF
+        del self._b[: self._i]
+        self._boff += self._i
+        self._i = 0
+        room = self.BufferSize if not self._b else 1024
+        if hasattr(self.Reader, "read_go"):
+            data, err = self.Reader.read_go(room)
+        else:
+            data = self.Reader.read(room)
+            err = EOF if not data else OK
+        self._b += data
+        if data and err == EOF:
+            err = OK
+        return err
+
+
+def NewReader(r, device: int = 0) -> Reader:
+    return Reader(r=r, device=device)
+
+
+def NewReaderBytes(b: bytes, device: int = 0) -> Reader:
+    return Reader(b=b, device=device)
+
+
+# ---------------------------------------------------------------- batches
+
+
+class _Batch(C.Structure):
+    _fields_ = [
+        ("in_", C.c_void_p),
+        ("in_off", C.c_void_p),
+        ("out", C.c_void_p),
+        ("out_off", C.c_void_p),
+        ("out_size", C.c_void_p),
+        ("status", C.c_void_p),
+        ("count", C.c_uint64),
+        ("max_len", C.c_uint64),
+    ]
+
+
+def _stream_ptr(stream) -> int:
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return int(s.cuda_stream)
+
+
+def _need_cuda(*ts) -> None:
+    for t in ts:
+        if not t.is_cuda:
+            raise DeviceError(EDEVICE)
+
+
+@dataclass
+class CompressedBatch:
+    slots: "object"       # uint8 CUDA tensor
+    slot_off: "object"    # int64 CUDA tensor, count+1
+    sizes: "object"       # int64 CUDA tensor, count
+    status: "object"      # int32 CUDA tensor, count
+
+
+def slot_offsets(in_off, extra: int = 0):
+    """Slot offsets with capacity ez_compress_bound(n) per stream (device)."""
+    import torch
+
+    n = in_off[1:] - in_off[:-1]
+    cap = n + (n >> 2) + 32 + extra
+    cap = (cap + 15) & ~15
+    return torch.cat([torch.zeros(1, dtype=torch.int64, device=in_off.device), torch.cumsum(cap, 0)])
+
+
+def compress_batch(data, in_off, block: int = MiB, htable: int = 1024, max_len: int | None = None,
+                   append_magic: bool = True, slot_off=None, out: CompressedBatch | None = None,
+                   stream=None) -> CompressedBatch:
+    """K1: compress independent streams data[in_off[s]:in_off[s+1]] (CUDA tensors)."""
+    import torch
+
+    _need_cuda(data, in_off)
+    count = in_off.numel() - 1
+    if out is None:
+        if slot_off is None:
+            slot_off = slot_offsets(in_off)
+        total = int(slot_off[-1].item())
+        out = CompressedBatch(
+            torch.empty(total + 16, dtype=torch.uint8, device=data.device),
+            slot_off,
+            torch.empty(count, dtype=torch.int64, device=data.device),
+            torch.empty(count, dtype=torch.int32, device=data.device),
+        )
+    if max_len is None:
+        max_len = int((in_off[1:] - in_off[:-1]).max().item()) if count else 0
+    b = _Batch(data.data_ptr(), in_off.data_ptr(), out.slots.data_ptr(), out.slot_off.data_ptr(),
+               out.sizes.data_ptr(), out.status.data_ptr(), count, max_len)
+    flags = 0 if append_magic else F_NO_MAGIC
+    _check(_lib().ez_compress_batch(block, htable, flags, C.byref(b), _stream_ptr(stream)))
+    return out
+
+
+def pack(cb: CompressedBatch, packed=None, packed_off=None, workspace=None, stream=None):
+    """K3: dense packing of the compressed slots -> (packed, packed_off)."""
+    import torch
+
+    count = cb.sizes.numel()
+    dev = cb.slots.device
+    if packed is None:
+        packed = torch.empty(cb.slots.numel(), dtype=torch.uint8, device=dev)
+    if packed_off is None:
+        packed_off = torch.empty(count + 1, dtype=torch.int64, device=dev)
+    if workspace is None:
+        workspace = torch.empty(_lib().ez_pack_workspace(count), dtype=torch.uint8, device=dev)
+    _check(_lib().ez_pack_batch(cb.slots.data_ptr(), cb.slot_off.data_ptr(), cb.sizes.data_ptr(), count,
+                                packed.data_ptr(), packed_off.data_ptr(), workspace.data_ptr(), _stream_ptr(stream)))
+    return packed, packed_off
+
+
+def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=None, sizes=None, status=None,
+                     stream=None):
+    """K2: decode complete streams comp[comp_off[s]:comp_off[s+1]] into
+    out[out_off[s]:out_off[s+1]] -> (out, sizes, status)."""
+    import torch
+
+    _need_cuda(comp, comp_off, out_off)
+    count = comp_off.numel() - 1
+    dev = comp.device
+    if out is None:
+        out = torch.empty(int(out_off[-1].item()) + 16, dtype=torch.uint8, device=dev)
+    if sizes is None:
+        sizes = torch.empty(count, dtype=torch.int64, device=dev)
+    if status is None:
+        status = torch.empty(count, dtype=torch.int32, device=dev)
+    b = _Batch(comp.data_ptr(), comp_off.data_ptr(), out.data_ptr(), out_off.data_ptr(), sizes.data_ptr(),
+               status.data_ptr(), count, 0)
+    _check(_lib().ez_decompress_batch(block_size_limit, C.byref(b), _stream_ptr(stream)))
+    return out, sizes, status

@@ -1,0 +1,522 @@
+// ez_capi.hip — implementation of include/eazy.h over the gfx950 kernels.
+//
+// Host-side responsibilities only: argument validation (the reference's
+// panics), HBM buffer management for the streaming handles, H2D/D2H of the
+// handles' per-call data, and kernel launches.  All compression and
+// decompression runs in K1/K2/K3; there is no CPU code path for them.
+#include <hip/hip_runtime.h>
+
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include "ez_format.h"
+#include "ez_internal.h"
+
+namespace {
+
+int g_device_count = -1;
+std::mutex g_mu;
+
+int device_count() {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (g_device_count < 0) {
+        int n = 0;
+        if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+        g_device_count = n;
+    }
+    return g_device_count;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    bool ok = false;
+    explicit DeviceGuard(int dev) {
+        if (device_count() <= 0) return;
+        if (hipGetDevice(&prev) != hipSuccess) return;
+        if (dev >= 0 && dev != prev && hipSetDevice(dev) != hipSuccess) return;
+        ok = true;
+    }
+    ~DeviceGuard() {
+        if (ok && prev >= 0) (void)hipSetDevice(prev);
+    }
+};
+
+#define EZ_HIP(x)                                   \
+    do {                                            \
+        if ((x) != hipSuccess) return EZ_EDEVICE;   \
+    } while (0)
+
+// grow-only device buffer
+struct DBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return EZ_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = n < 4096 ? 4096 : n + n / 4;
+        if (hipMalloc(&p, c) != hipSuccess) return EZ_EDEVICE;
+        cap = c;
+        return EZ_OK;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const { return (T *)p; }
+};
+
+bool pow2(int64_t x) { return x > 0 && (x & (x - 1)) == 0; }
+
+// Writer.init size checks (writer.go:161-169)
+bool valid_writer_sizes(int64_t bs, int64_t hs) {
+    if (!pow2(bs) || bs < 32 || bs > ((int64_t)1 << 31)) return false;
+    if (!pow2(hs) || hs < 4) return false;
+    return true;
+}
+
+// appendHeader writer.go:495-517
+size_t header_bytes(uint8_t *b, int append_magic, int ver, int64_t bs) {
+    size_t k = 0;
+    if (append_magic) {
+        const uint8_t m[6] = {0x80, 0x02, 'e', 'a', 'z', 'y'};
+        memcpy(b, m, 6);
+        k = 6;
+    }
+    if (ver != 0) {
+        b[k++] = 0x80; b[k++] = 0x08; b[k++] = (uint8_t)ver;
+    }
+    b[k++] = 0x80; b[k++] = 0x10; b[k++] = (uint8_t)__builtin_ctzll((uint64_t)bs);
+    return k;
+}
+
+// per-device scratch for batch compression with large hash tables
+struct Scratch {
+    DBuf ht;
+};
+std::vector<Scratch> g_scratch;
+
+}  // namespace
+
+// ------------------------------------------------------------------ misc
+
+extern "C" const char *ez_strerror(int code) {
+    switch (code) {
+    case EZ_OK: return "ok";
+    case EZ_EOF: return "EOF";
+    case EZ_ESHORTBUF: return "short buffer";
+    case EZ_EUNEXPECTEDEOF: return "unexpected EOF";
+    case EZ_EOVERFLOW: return "length/offset overflow";
+    case EZ_EBADMAGIC: return "bad magic";
+    case EZ_ENOMAGIC: return "no magic";
+    case EZ_EBLOCKLIMIT: return "block size is more than the limit";
+    case EZ_EUNSUPMETA: return "unsupported meta tag";
+    case EZ_EUNSUPVER: return "unsupported file format version";
+    case EZ_EBREAK: return "break point";
+    case EZ_EMISSEDMETA: return "missed meta";
+    case EZ_EINVAL: return "invalid argument (reference panic)";
+    case EZ_ESINK: return "underlying writer failed";
+    case EZ_ENOSPC: return "output buffer too small";
+    case EZ_EDEVICE: return "no usable MI355X device / HIP error";
+    case EZ_ESTUCK: return "kernel progress guard tripped";
+    default: return "unknown error";
+    }
+}
+
+extern "C" int ez_abi_version(void) { return EZ_ABI_VERSION; }
+extern "C" int ez_device_count(void) { return device_count(); }
+
+// ------------------------------------------------------------------ token codec
+
+extern "C" int ez_encode_tag(uint8_t *b, size_t cap, size_t *len, int tag, int64_t l) {
+    uint8_t t[16];
+    const int k = ez::enc_tag(t, tag, l);
+    if (k < 0) return EZ_EINVAL;
+    if (*len + (size_t)k > cap) return EZ_ENOSPC;
+    memcpy(b + *len, t, (size_t)k);
+    *len += (size_t)k;
+    return EZ_OK;
+}
+
+extern "C" int ez_encode_offset(uint8_t *b, size_t cap, size_t *len, int64_t off, int64_t l) {
+    uint8_t t[16];
+    const int k = ez::enc_offset(t, off, l);
+    if (k < 0) return EZ_EINVAL;
+    if (*len + (size_t)k > cap) return EZ_ENOSPC;
+    memcpy(b + *len, t, (size_t)k);
+    *len += (size_t)k;
+    return EZ_OK;
+}
+
+extern "C" int ez_encode_meta(uint8_t *b, size_t cap, size_t *len, int64_t meta, int64_t l) {
+    uint8_t t[16];
+    const int k = ez::enc_meta(t, meta, l);
+    if (k < 0) return EZ_EINVAL;
+    if (*len + (size_t)k > cap) return EZ_ENOSPC;
+    memcpy(b + *len, t, (size_t)k);
+    *len += (size_t)k;
+    return EZ_OK;
+}
+
+extern "C" int ez_decode_tag(const uint8_t *b, size_t n, size_t st, int *tag, int64_t *l, size_t *i) {
+    int64_t j;
+    const int e = ez::dec_tag(b, (int64_t)n, (int64_t)st, tag, l, &j);
+    *i = (size_t)j;
+    return e;
+}
+
+extern "C" int ez_decode_offset(const uint8_t *b, size_t n, size_t st, int64_t l, int64_t *off, size_t *i) {
+    int64_t j;
+    const int e = ez::dec_offset(b, (int64_t)n, (int64_t)st, l, off, &j);
+    *i = (size_t)j;
+    return e;
+}
+
+extern "C" int ez_decode_meta(const uint8_t *b, size_t n, size_t st, int64_t *meta, int64_t *l, size_t *i) {
+    int64_t j;
+    const int e = ez::dec_meta(b, (int64_t)n, (int64_t)st, meta, l, &j);
+    *i = (size_t)j;
+    return e;
+}
+
+extern "C" size_t ez_compress_bound(size_t n) { return (size_t)ez::compress_bound(n); }
+
+// ------------------------------------------------------------------ Writer handle
+
+struct ez_writer {
+    int device = 0;
+    int64_t bs = 0, hs = 0;
+    int append_magic = 1;
+    int ver = 0;
+    bool pristine = true;  // isreset(): nothing emitted since the last reset
+    int64_t pos = 0;       // w.pos
+    DBuf ring, ht, in, out, meta;
+    hipStream_t stream = nullptr;
+};
+
+namespace {
+
+int writer_zero(ez_writer *w) {
+    EZ_HIP(hipMemsetAsync(w->ring.p, 0, (size_t)w->bs, w->stream));
+    EZ_HIP(hipMemsetAsync(w->ht.p, 0, (size_t)w->hs * 4, w->stream));
+    EZ_HIP(hipStreamSynchronize(w->stream));
+    w->pos = 0;
+    w->pristine = true;
+    return EZ_OK;
+}
+
+int writer_alloc(ez_writer *w, int64_t bs, int64_t hs) {
+    if (w->ring.ensure((size_t)bs)) return EZ_EDEVICE;
+    if (w->ht.ensure((size_t)hs * 4)) return EZ_EDEVICE;
+    w->bs = bs;
+    w->hs = hs;
+    return EZ_OK;
+}
+
+}  // namespace
+
+extern "C" int ez_writer_new(int64_t block, int64_t htable, int device, ez_writer **out) {
+    *out = nullptr;
+    if (!valid_writer_sizes(block, htable)) return EZ_EINVAL;
+    DeviceGuard g(device);
+    if (!g.ok) return EZ_EDEVICE;
+    ez_writer *w = new ez_writer();
+    w->device = device;
+    if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete w;
+        return EZ_EDEVICE;
+    }
+    int e = writer_alloc(w, block, htable);
+    if (!e) e = writer_zero(w);
+    if (e) {
+        ez_writer_free(w);
+        return e;
+    }
+    *out = w;
+    return EZ_OK;
+}
+
+extern "C" void ez_writer_free(ez_writer *w) {
+    if (!w) return;
+    DeviceGuard g(w->device);
+    w->ring.release();
+    w->ht.release();
+    w->in.release();
+    w->out.release();
+    w->meta.release();
+    if (w->stream) (void)hipStreamDestroy(w->stream);
+    delete w;
+}
+
+extern "C" int ez_writer_set_append_magic(ez_writer *w, int on) {
+    w->append_magic = on ? 1 : 0;
+    return EZ_OK;
+}
+
+extern "C" int ez_writer_set_version(ez_writer *w, int ver) {
+    w->ver = ver;
+    return EZ_OK;
+}
+
+extern "C" int ez_writer_is_reset(const ez_writer *w) { return w->pristine ? 1 : 0; }
+
+extern "C" int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t *out, size_t cap, size_t *out_n) {
+    *out_n = 0;
+    DeviceGuard g(w->device);
+    if (!g.ok) return EZ_EDEVICE;
+    const size_t bound = ez_compress_bound(n);
+    if (w->in.ensure(n + 16) || w->out.ensure(bound + 16) || w->meta.ensure(64)) return EZ_EDEVICE;
+    // meta: in_off[2] out_off[2] out_size[1] status[1]
+    uint64_t m[6] = {0, (uint64_t)n, 0, (uint64_t)bound, 0, 0};
+    if (n) EZ_HIP(hipMemcpyAsync(w->in.p, p, n, hipMemcpyHostToDevice, w->stream));
+    EZ_HIP(hipMemcpyAsync(w->meta.p, m, sizeof(m), hipMemcpyHostToDevice, w->stream));
+    ez::CompressArgs a{};
+    uint64_t *dm = w->meta.as<uint64_t>();
+    a.in = w->in.as<uint8_t>();
+    a.in_off = dm;
+    a.out = w->out.as<uint8_t>();
+    a.out_off = dm + 2;
+    a.out_size = dm + 4;
+    a.status = (int32_t *)(dm + 5);
+    a.count = 1;
+    a.bs = w->bs;
+    a.hs = w->hs;
+    a.append_magic = w->append_magic;
+    a.ver = w->ver;
+    a.header = w->pristine ? 1 : 0;
+    a.start = w->pos;
+    a.ring = w->ring.as<uint8_t>();
+    a.ht_global = w->ht.as<uint32_t>();
+    a.max_len = n ? n : 1;
+    EZ_HIP(ez::launch_compress(a, w->stream));
+    EZ_HIP(hipMemcpyAsync(m, w->meta.p, sizeof(m), hipMemcpyDeviceToHost, w->stream));
+    EZ_HIP(hipStreamSynchronize(w->stream));
+    const int st = (int)(int32_t)(m[5] & 0xffffffffu);
+    if (st) return st;
+    const size_t got = (size_t)m[4];
+    if (got > cap) return EZ_ENOSPC;
+    if (got) {
+        EZ_HIP(hipMemcpyAsync(out, w->out.p, got, hipMemcpyDeviceToHost, w->stream));
+        EZ_HIP(hipStreamSynchronize(w->stream));
+    }
+    w->pos += (int64_t)n;
+    w->pristine = false;
+    *out_n = got;
+    return EZ_OK;
+}
+
+extern "C" int ez_writer_header(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n) {
+    *out_n = 0;
+    if (!w->pristine) return EZ_OK;
+    uint8_t h[16];
+    const size_t k = header_bytes(h, w->append_magic, w->ver, w->bs);
+    if (k > cap) return EZ_ENOSPC;
+    memcpy(out, h, k);
+    *out_n = k;
+    w->pristine = false;
+    return EZ_OK;
+}
+
+extern "C" int ez_writer_break(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n) {
+    *out_n = 0;
+    uint8_t h[32];
+    size_t k = 0;
+    if (w->pristine) k = header_bytes(h, w->append_magic, w->ver, w->bs);
+    h[k++] = 0x80;
+    h[k++] = 0x18 | 7;  // Meta, MetaBreak|MetaLen0 (writer.go:363)
+    if (k > cap) return EZ_ENOSPC;
+    memcpy(out, h, k);
+    *out_n = k;
+    w->pristine = false;
+    return EZ_OK;
+}
+
+extern "C" int ez_writer_reset(ez_writer *w) {
+    DeviceGuard g(w->device);
+    if (!g.ok) return EZ_EDEVICE;
+    return writer_zero(w);
+}
+
+extern "C" int ez_writer_reset_size(ez_writer *w, int64_t block, int64_t htable) {
+    if (!valid_writer_sizes(block, htable)) return EZ_EINVAL;
+    DeviceGuard g(w->device);
+    if (!g.ok) return EZ_EDEVICE;
+    int e = writer_alloc(w, block, htable);
+    if (e) return e;
+    return writer_zero(w);
+}
+
+// ------------------------------------------------------------------ Reader handle
+
+struct ez_reader {
+    int device = 0;
+    ez::DecodeState st{};
+    int64_t limit = 0;
+    int require_magic = 0, skip_meta = 0;
+    DBuf in, out, win, tmp, dstate, meta;
+    hipStream_t stream = nullptr;
+};
+
+extern "C" int ez_reader_new(int device, ez_reader **out) {
+    *out = nullptr;
+    DeviceGuard g(device);
+    if (!g.ok) return EZ_EDEVICE;
+    ez_reader *r = new ez_reader();
+    r->device = device;
+    if (hipStreamCreateWithFlags(&r->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete r;
+        return EZ_EDEVICE;
+    }
+    if (r->dstate.ensure(sizeof(ez::DecodeState)) || r->meta.ensure(64)) {
+        ez_reader_free(r);
+        return EZ_EDEVICE;
+    }
+    *out = r;
+    return EZ_OK;
+}
+
+extern "C" void ez_reader_free(ez_reader *r) {
+    if (!r) return;
+    DeviceGuard g(r->device);
+    r->in.release();
+    r->out.release();
+    r->win.release();
+    r->tmp.release();
+    r->dstate.release();
+    r->meta.release();
+    if (r->stream) (void)hipStreamDestroy(r->stream);
+    delete r;
+}
+
+extern "C" int ez_reader_configure(ez_reader *r, int64_t block_size_limit, int require_magic, int skip_meta) {
+    r->limit = block_size_limit;
+    r->require_magic = require_magic ? 1 : 0;
+    r->skip_meta = skip_meta ? 1 : 0;
+    return EZ_OK;
+}
+
+// ResetBytes reader.go:102-113: block = block[:0], pos = 0, state = 0
+// (r.d.Ver is kept, as in the reference).
+extern "C" int ez_reader_reset(ez_reader *r) {
+    const int32_t ver = r->st.ver;
+    r->st = ez::DecodeState{};
+    r->st.ver = ver;
+    return EZ_OK;
+}
+
+extern "C" int ez_reader_pending(const ez_reader *r) { return r->st.state != 0 ? 1 : 0; }
+
+extern "C" int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size_t i, int64_t boff, uint8_t *p,
+                              size_t p_len, size_t *n, size_t *i_out, int64_t *detail) {
+    *n = 0;
+    *i_out = i;
+    if (detail) *detail = 0;
+    if (p_len == 0) return EZ_OK;  // Read(p) with len(p) == 0 returns at once (reader.go:119)
+    DeviceGuard g(r->device);
+    if (!g.ok) return EZ_EDEVICE;
+    const size_t H = (size_t)r->st.hist;
+    if (r->in.ensure(b_len + 16) || r->out.ensure(H + p_len + 16) || r->meta.ensure(64)) return EZ_EDEVICE;
+    if (b_len) EZ_HIP(hipMemcpyAsync(r->in.p, b, b_len, hipMemcpyHostToDevice, r->stream));
+    if (H) EZ_HIP(hipMemcpyAsync(r->out.p, r->win.p, H, hipMemcpyDeviceToDevice, r->stream));
+    r->st.i = (int64_t)i;
+    EZ_HIP(hipMemcpyAsync(r->dstate.p, &r->st, sizeof(r->st), hipMemcpyHostToDevice, r->stream));
+    uint64_t m[4] = {0, (uint64_t)b_len, (uint64_t)H, (uint64_t)(H + p_len)};
+    EZ_HIP(hipMemcpyAsync(r->meta.p, m, sizeof(m), hipMemcpyHostToDevice, r->stream));
+    ez::DecompressArgs a{};
+    uint64_t *dm = r->meta.as<uint64_t>();
+    a.in = r->in.as<uint8_t>();
+    a.in_off = dm;
+    a.out = r->out.as<uint8_t>();
+    a.out_off = dm + 2;
+    a.out_size = nullptr;
+    a.status = nullptr;
+    a.count = 1;
+    a.block_size_limit = r->limit;
+    a.require_magic = r->require_magic;
+    a.skip_unsupported_meta = r->skip_meta;
+    a.handle = 1;
+    a.boff = boff;
+    a.st = r->dstate.as<ez::DecodeState>();
+    EZ_HIP(ez::launch_decompress(a, r->stream));
+    EZ_HIP(hipMemcpyAsync(&r->st, r->dstate.p, sizeof(r->st), hipMemcpyDeviceToHost, r->stream));
+    EZ_HIP(hipStreamSynchronize(r->stream));
+    const size_t got = (size_t)r->st.n;
+    const size_t H2 = (size_t)r->st.hist;
+    // keep the last min(pos, bs) bytes of the current block as history
+    if (H2) {
+        if (r->tmp.ensure(H2) || r->win.ensure(H2)) return EZ_EDEVICE;
+        EZ_HIP(hipMemcpyAsync(r->tmp.p, r->out.as<uint8_t>() + H + got - H2, H2, hipMemcpyDeviceToDevice, r->stream));
+        EZ_HIP(hipMemcpyAsync(r->win.p, r->tmp.p, H2, hipMemcpyDeviceToDevice, r->stream));
+    }
+    if (got) EZ_HIP(hipMemcpyAsync(p, r->out.as<uint8_t>() + H, got, hipMemcpyDeviceToHost, r->stream));
+    EZ_HIP(hipStreamSynchronize(r->stream));
+    *n = got;
+    *i_out = (size_t)r->st.i;
+    if (detail) *detail = r->st.detail;
+    return r->st.err;
+}
+
+// ------------------------------------------------------------------ batches
+
+extern "C" int ez_compress_batch(int64_t block, int64_t htable, int flags, const ez_batch *b, void *hip_stream) {
+    if (!valid_writer_sizes(block, htable)) return EZ_EINVAL;
+    if (device_count() <= 0) return EZ_EDEVICE;
+    ez::CompressArgs a{};
+    a.in = b->in;
+    a.in_off = b->in_off;
+    a.out = b->out;
+    a.out_off = b->out_off;
+    a.out_size = b->out_size;
+    a.status = b->status;
+    a.count = b->count;
+    a.bs = block;
+    a.hs = htable;
+    a.append_magic = (flags & EZ_F_NO_MAGIC) ? 0 : 1;
+    a.ver = 0;
+    a.header = 1;
+    a.start = 0;
+    a.ring = nullptr;
+    a.max_len = b->max_len;
+    const uint64_t words = ez::compress_scratch_words(b->count, htable);
+    if (words) {
+        int dev = 0;
+        EZ_HIP(hipGetDevice(&dev));
+        std::lock_guard<std::mutex> lk(g_mu);
+        if ((int)g_scratch.size() <= dev) g_scratch.resize((size_t)dev + 1);
+        if (g_scratch[(size_t)dev].ht.ensure((size_t)words * 4)) return EZ_EDEVICE;
+        a.ht_global = g_scratch[(size_t)dev].ht.as<uint32_t>();
+    }
+    EZ_HIP(ez::launch_compress(a, (hipStream_t)hip_stream));
+    return EZ_OK;
+}
+
+extern "C" size_t ez_pack_workspace(uint64_t count) { return ez::pack_workspace(count); }
+
+extern "C" int ez_pack_batch(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
+                             uint8_t *packed, uint64_t *packed_off, void *workspace, void *hip_stream) {
+    if (device_count() <= 0) return EZ_EDEVICE;
+    EZ_HIP(ez::launch_pack(slots, slot_off, sizes, count, packed, packed_off, workspace, (hipStream_t)hip_stream));
+    return EZ_OK;
+}
+
+extern "C" int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *hip_stream) {
+    if (device_count() <= 0) return EZ_EDEVICE;
+    ez::DecompressArgs a{};
+    a.in = b->in;
+    a.in_off = b->in_off;
+    a.out = b->out;
+    a.out_off = b->out_off;
+    a.out_size = b->out_size;
+    a.status = b->status;
+    a.count = b->count;
+    a.block_size_limit = block_size_limit;
+    a.handle = 0;
+    EZ_HIP(ez::launch_decompress(a, (hipStream_t)hip_stream));
+    return EZ_OK;
+}

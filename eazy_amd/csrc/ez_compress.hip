@@ -1,0 +1,438 @@
+// ez_compress.hip — K1: bit-exact eazy compression on gfx950.
+//
+// Restates Writer.Write (writer.go:206-337) with writeRunlen (:441-489),
+// writeZeros (:407-439), hash (:491-493), the header (:495-517) and the
+// Encoder (:537-597).  One wave64 per stream.
+//
+// Speculative window parse: the greedy loop visits position
+// i, inserts ht[hash(i)] = start+i and judges the previous entry.  Judging
+// depends only on (done, w.pos, ring, ht-before-insert), and none of these
+// change until the first ACCEPT.  So the wave judges 64 consecutive
+// positions at once:
+//   * lane j hashes position i+j; its candidate is the latest earlier lane
+//     of the window with the same hash (an LDS bucket mask + exact check),
+//     else ht[hash];
+//   * every lane evaluates its branch (far skip / runlen / zero run / cut /
+//     window match) with extensions capped at kCap bytes — acceptance is
+//     monotone in the extension lengths, so a capped result is either a
+//     certain reject, a certain accept, or "maybe";
+//   * the first lane that can accept is resolved exactly with wave-wide
+//     64-byte extension steps (ballot + ctz); if it rejects, the next one;
+//   * hash inserts of lanes <= a are applied last-writer-wins, then lane a's
+//     action is emitted and the next window starts at the new i (which may
+//     be smaller than before: SURVEY A.7).
+// The ring (block) is never materialised for fresh streams: a linear view
+// reproduces block[x & mask] exactly:
+//   q = w.pos - bs + ((x - w.pos) mod bs);  byte = q >= start ? p[q-start]
+//                                                  : (ring ? ring[q & mask] : 0)
+#include "ez_format.h"
+#include "ez_internal.h"
+#include "ez_wave.h"
+
+namespace ez {
+namespace {
+
+constexpr int kCap = 8;          // per-lane speculative extension cap (>= kMinCopyChunk)
+constexpr int kBuckets = 256;    // intra-window hash bucket masks
+constexpr int kMaskBytes = kBuckets * 8;
+constexpr int kHashBytes = kWave * 4;
+constexpr int64_t kPLdsMax = 16 * 1024;  // stage streams up to this size in LDS
+constexpr int64_t kHtLdsMax = 4096;      // hash tables up to this many entries in LDS
+
+enum Kind : int { kReject = 0, kWin = 1, kRun = 2, kCut = 3, kZero = 4 };
+
+// Stream input view: LDS-staged (PL) or global.
+template <bool PL>
+struct InView {
+    const uint8_t *g;      // global bytes of the stream
+    const uint32_t *gw;    // global aligned words covering g
+    uint64_t gr;           // g - gw (bytes)
+    uint64_t glast;        // last valid word index of gw
+    const uint32_t *lw;    // LDS words (PL)
+    uint32_t lr;           // byte misalignment inside lw (PL)
+
+    __device__ __forceinline__ uint32_t b(int64_t x) const {
+        if (PL) return ((const uint8_t *)lw)[lr + (uint64_t)x];
+        return g[x];
+    }
+    __device__ __forceinline__ uint32_t u32(int64_t x) const {
+        if (PL) return words_u32(lw, lr + (uint64_t)x);
+        const uint64_t a = gr + (uint64_t)x;
+        const uint64_t k = a >> 2;
+        const uint32_t w0 = gw[k];
+        const uint32_t w1 = gw[k + 1 <= glast ? k + 1 : glast];
+        return __builtin_amdgcn_alignbyte(w1, w0, (uint32_t)(a & 3));
+    }
+};
+
+struct OutBuf {
+    uint8_t *p;
+    int64_t cap;
+    int64_t op;
+    int err;
+};
+
+__device__ __forceinline__ void put_hdr(OutBuf &o, const Hdr &h, int lane) {
+    if (o.err) return;
+    if (o.op + h.n > o.cap) { o.err = EZ_ENOSPC; return; }
+    if (lane < h.n) o.p[o.op + lane] = h.byte(lane);
+    o.op += h.n;
+}
+
+template <class V>
+__device__ __forceinline__ void put_bytes(OutBuf &o, const V &P, int64_t src, int64_t L, int lane) {
+    if (o.err) return;
+    if (o.op + L > o.cap) { o.err = EZ_ENOSPC; return; }
+    uint8_t *d = o.p + o.op;
+    for (int64_t k = lane; k < L; k += kWave) d[k] = (uint8_t)P.b(src + k);
+    o.op += L;
+}
+
+// appendLiteral writer.go:519-522
+template <class V>
+__device__ __forceinline__ void put_literal(OutBuf &o, const V &P, int64_t st, int64_t end, int lane) {
+    Hdr h;
+    if (!hdr_tag(h, kLiteral, end - st)) { o.err = EZ_EINVAL; return; }
+    put_hdr(o, h, lane);
+    put_bytes(o, P, st, end - st, lane);
+}
+
+// Wave-cooperative extension: number of consecutive m >= from with ok(m).
+template <class F>
+__device__ __forceinline__ int64_t coop_count(int64_t from, int lane, F ok) {
+    int64_t base = from;
+    for (;;) {
+        const uint64_t bad = wballot(!ok(base + lane));
+        if (bad) return base + ffs64(bad);
+        base += kWave;
+    }
+}
+
+template <bool PL, bool HTL, bool RING>
+__device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem) {
+    const int lane = lane_id();
+    const uint64_t ib = A.in_off[s];
+    const int64_t n = (int64_t)(A.in_off[s + 1] - ib);
+    const int64_t bs = A.bs, mask = bs - 1;
+    const int64_t hs = A.hs;
+    const unsigned hsh = 32u - (unsigned)(64 - __builtin_clzll((uint64_t)(hs - 1)));
+    const int64_t start = A.start;
+    const uint8_t *ring = A.ring;
+
+    // ---- LDS carve (all offsets 16-aligned)
+    const uint64_t ht_bytes = HTL ? (uint64_t)hs * 4 : 0;
+    uint64_t *bmask = (uint64_t *)(smem + ht_bytes);
+    uint32_t *H = (uint32_t *)(smem + ht_bytes + kMaskBytes);
+    uint32_t *lw = (uint32_t *)(smem + ht_bytes + kMaskBytes + kHashBytes);
+    uint32_t *ht;
+    if (HTL) ht = (uint32_t *)smem;
+    else ht = RING ? A.ht_global : A.ht_global + (uint64_t)blockIdx.x * (uint64_t)hs;
+
+    // ---- input view (+ LDS staging)
+    InView<PL> P;
+    P.g = A.in + ib;
+    P.gr = (uint64_t)(uintptr_t)P.g & 3;
+    P.gw = (const uint32_t *)(P.g - P.gr);
+    P.glast = (P.gr + (uint64_t)n + 3) / 4;
+    P.glast = P.glast ? P.glast - 1 : 0;
+    P.lw = lw;
+    P.lr = (uint32_t)P.gr;
+    if (PL) {
+        const uint64_t nw = (P.gr + (uint64_t)n + 3) / 4;
+        for (uint64_t k = lane; k < nw; k += kWave) lw[k] = P.gw[k];
+        if (lane < 4) lw[nw + lane] = 0;
+    }
+    // ---- hash table and bucket masks
+    if (HTL) {
+        if (RING) for (int64_t k = lane; k < hs; k += kWave) ht[k] = A.ht_global[k];
+        else for (int64_t k = lane; k < hs; k += kWave) ht[k] = 0;
+    } else if (!RING) {
+        for (int64_t k = lane; k < hs; k += kWave) ht[k] = 0;
+    }
+    for (int k = lane; k < kBuckets; k += kWave) bmask[k] = 0;
+    __syncthreads();
+
+    OutBuf o;
+    o.p = A.out + A.out_off[s];
+    o.cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    o.op = 0;
+    o.err = 0;
+
+    // ---- header (writer.go:207-209, 495-517)
+    if (A.header) {
+        Hdr h;
+        if (A.append_magic) { h.put(0x80); h.put(0x02); h.put('e'); h.put('a'); h.put('z'); h.put('y'); }
+        if (A.ver != 0) { h.put(0x80); h.put(0x08); h.put((uint32_t)A.ver); }
+        h.put(0x80); h.put(0x10); h.put((uint32_t)__builtin_ctzll((uint64_t)bs));
+        put_hdr(o, h, lane);
+    }
+
+    // block[y & mask] as seen while w.pos == wpos
+    auto ringb = [&](int64_t y, int64_t wpos) -> uint32_t {
+        const int64_t q = wpos - bs + ((y - wpos) & mask);
+        if (q >= start) return P.b(q - start);
+        if (RING) return ring[q & mask];
+        return 0u;
+    };
+
+    int64_t done = 0, i = 0;
+    int64_t guard = 0;
+    const int64_t guard_max = 16 * n + 4096;
+
+    while (i + 4 <= n && !o.err) {
+        if (++guard > guard_max) { o.err = EZ_ESTUCK; break; }
+        const int64_t wpos = start + done;
+        const int64_t rem = n - 3 - i;
+        const int nvalid = rem < kWave ? (int)rem : kWave;
+        const int64_t x = i + lane;
+        const bool valid = lane < nvalid;
+
+        // -- hash + intra-window predecessor / successor with the same hash
+        uint32_t h = 0xffffffffu;
+        if (valid) h = (P.u32(x) * kHashMul) >> hsh;
+        const int bk = (int)(h & (kBuckets - 1));
+        if (valid) {
+            atomicOr((unsigned long long *)&bmask[bk], 1ull << lane);
+            H[lane] = h;
+        }
+        __syncthreads();
+        int prev = -1, next = kWave;
+        if (valid) {
+            const uint64_t m = bmask[bk];
+            uint64_t below = m & ((1ull << lane) - 1);
+            while (below) {
+                const int k = 63 - __builtin_clzll(below);
+                if (H[k] == h) { prev = k; break; }
+                below &= ~(1ull << k);
+            }
+            uint64_t above = lane == 63 ? 0ull : (m & (~0ull << (lane + 1)));
+            while (above) {
+                const int k = __builtin_ctzll(above);
+                if (H[k] == h) { next = k; break; }
+                above &= above - 1;
+            }
+        }
+        int64_t cand = 0;
+        if (valid) cand = prev >= 0 ? (int64_t)(uint32_t)(start + i + prev) : (int64_t)ht[h];
+
+        // -- per-lane capped evaluation
+        int kind = kReject;
+        bool exact = true;
+        int64_t v_st = 0, v_ist = 0, v_iend = 0;
+        if (valid) {
+            const int64_t off = cand - wpos;
+            if (-off > bs) {
+                kind = kReject;  // far skip (writer.go:221-224)
+            } else if (off >= 0 && x > done + off) {
+                // runlen (writer.go:227-231 -> writeRunlen :441-489)
+                const int64_t st = done + off;
+                v_st = st;
+                if (st + 8 < n && P.u32(st) == 0 && P.u32(st + 4) == 0) {
+                    kind = kZero;
+                } else {
+                    int f = 0;
+                    while (f < kCap && x + f < n && P.b(st + f) == P.b(x + f)) f++;
+                    int c = 0;
+                    while (c < kCap && st - 1 - c >= 0 && x - 1 - c >= done && P.b(st - 1 - c) == P.b(x - 1 - c)) c++;
+                    const bool capped = f == kCap || c == kCap;
+                    if (!capped && f + c < kMinCopyChunk) kind = kReject;
+                    else if (x - st >= bs - 8) kind = kCut;
+                    else { kind = kRun; exact = !capped; v_ist = x - c; v_iend = x + f; }
+                }
+            } else {
+                // window match (writer.go:233-301)
+                int64_t ist = x - 1, st = cand - 1;
+                int c = 0;
+                while (c < kCap && ist >= done && P.b(ist) == ringb(st, wpos)) { ist--; st--; c++; }
+                ist++; st++;
+                int64_t iend = x, end = cand;
+                int f = 0;
+                while (f < kCap && iend < n && P.b(iend) == ringb(end, wpos)) { iend++; end++; f++; }
+                const bool capped = c == kCap || f == kCap;
+                const int64_t blit = wpos - bs;
+                const int64_t bend = blit + (iend - done);
+                int64_t d = bend - st;
+                if (d > 0) { end -= d; iend -= d; }
+                d = (end - bs) - blit;
+                if (d > 0) { end -= d; iend -= d; }
+                if (end - st >= kMinCopyChunk) { kind = kWin; exact = !capped; v_ist = ist; v_iend = iend; }
+                else if (capped) { kind = kWin; exact = false; }
+                else kind = kReject;
+            }
+        }
+
+        // -- first lane that accepts (exact resolution, wave-wide)
+        uint64_t cm = wballot(valid && kind != kReject);
+        const uint64_t exm = wballot(exact);
+        int a = -1, ka = kReject;
+        int64_t xa = 0, sta = 0, ista = 0, ienda = 0, canda = 0;
+        while (cm) {
+            const int l = ffs64(cm);
+            const int kl = rl32(kind, l);
+            const bool ex = (exm >> l) & 1;
+            const int64_t xl = i + l;
+            if (kl == kWin) {
+                const int64_t cl = rl64(cand, l);
+                int64_t ist, iend;
+                if (ex) {
+                    ist = rl64(v_ist, l);
+                    iend = rl64(v_iend, l);
+                } else {
+                    const int64_t bw = coop_count(0, lane, [&](int64_t m) {
+                        return xl - 1 - m >= done && P.b(xl - 1 - m) == ringb(cl - 1 - m, wpos);
+                    });
+                    const int64_t fw = coop_count(0, lane, [&](int64_t m) {
+                        return xl + m < n && P.b(xl + m) == ringb(cl + m, wpos);
+                    });
+                    ist = xl - bw;
+                    int64_t st = cl - bw;
+                    iend = xl + fw;
+                    int64_t end = cl + fw;
+                    const int64_t blit = wpos - bs;
+                    const int64_t bend = blit + (iend - done);
+                    int64_t d = bend - st;
+                    if (d > 0) { end -= d; iend -= d; }
+                    d = (end - bs) - blit;
+                    if (d > 0) { end -= d; iend -= d; }
+                    if (end - st < kMinCopyChunk) { cm &= cm - 1; continue; }  // maybe -> reject
+                }
+                a = l; ka = kWin; xa = xl; canda = cl; ista = ist; ienda = iend;
+                break;
+            }
+            a = l; ka = kl; xa = xl; sta = rl64(v_st, l);
+            if (kl == kRun) {
+                if (ex) {
+                    ista = rl64(v_ist, l);
+                    ienda = rl64(v_iend, l);
+                } else {
+                    const int64_t jf = coop_count(0, lane, [&](int64_t m) {
+                        return xl + m < n && P.b(sta + m) == P.b(xl + m);
+                    });
+                    const int64_t jb = coop_count(0, lane, [&](int64_t m) {
+                        return sta - 1 - m >= 0 && xl - 1 - m >= done && P.b(sta - 1 - m) == P.b(xl - 1 - m);
+                    });
+                    ista = xl - jb;
+                    ienda = xl + jf;
+                }
+            }
+            break;
+        }
+
+        // -- hash inserts of the visited lanes 0..last, last writer wins (writer.go:216-217)
+        const int last = a < 0 ? nvalid - 1 : a;
+        if (valid && lane <= last && next > last) ht[h] = (uint32_t)(start + x);
+        if (valid) bmask[bk] = 0;
+        __syncthreads();
+
+        if (a < 0) { i += nvalid; continue; }
+
+        // -- lane a's action
+        if (ka == kWin) {
+            // writer.go:303-321
+            if (done < ista) put_literal(o, P, done, ista, lane);
+            const int64_t dist = start + xa - canda;  // w.pos - st after the literal
+            const int64_t L = ienda - ista;
+            if (dist > bs) { o.err = EZ_EINVAL; break; }  // panic("too big offset")
+            Hdr hh;
+            if (!hdr_tag(hh, kCopy, L) || !hdr_offset(hh, dist, L)) { o.err = EZ_EINVAL; break; }
+            put_hdr(o, hh, lane);
+            if (xa + 1 + 4 <= n) {
+                const uint32_t h1 = (P.u32(xa + 1) * kHashMul) >> hsh;
+                if (lane == 0) ht[h1] = (uint32_t)(start + xa + 1);
+                __syncthreads();
+            }
+            i = ienda;
+            done = ienda;
+        } else if (ka == kRun) {
+            // writer.go:477-488 (the literal is unconditional: SURVEY A.6)
+            put_literal(o, P, done, ista, lane);
+            Hdr hh;
+            if (!hdr_tag(hh, kCopy, ienda - ista) || !hdr_offset(hh, xa - sta, ienda - ista)) { o.err = EZ_EINVAL; break; }
+            put_hdr(o, hh, lane);
+            i = ienda;
+            done = ienda;
+        } else if (ka == kCut) {
+            // writer.go:464-473
+            const int64_t iend = done + xa - sta;
+            put_literal(o, P, done, iend, lane);
+            i = iend;
+            done = iend;
+        } else {
+            // writeZeros writer.go:407-439, called with i = st
+            const int64_t zf = coop_count(0, lane, [&](int64_t m) { return sta + m < n && P.b(sta + m) == 0; });
+            const int64_t zb = coop_count(0, lane, [&](int64_t m) { return sta - 1 - m >= done && P.b(sta - 1 - m) == 0; });
+            const int64_t zi = sta - zb, ziend = sta + zf;
+            if (ziend - zi < kMinCopyChunk) {
+                i = zi + 1;  // unreachable: >= 8 zeros are guaranteed
+            } else {
+                if (done != zi) put_literal(o, P, done, zi, lane);
+                Hdr hh;
+                if (!hdr_tag(hh, kCopy, ziend - zi)) { o.err = EZ_EINVAL; break; }
+                hh.put(kOffLong);
+                hh.put(0);
+                put_hdr(o, hh, lane);
+                i = ziend;
+                done = ziend;
+            }
+        }
+    }
+    // trailing literal (writer.go:324-329)
+    if (!o.err && done < n) put_literal(o, P, done, n, lane);
+
+    if (RING) {
+        // copyData of this Write into the ring (writer.go:529-535), and
+        // the hash table back to HBM.
+        const int64_t k0 = n > bs ? n - bs : 0;
+        for (int64_t k = k0 + lane; k < n; k += kWave) A.ring[(start + k) & mask] = (uint8_t)P.b(k);
+        if (HTL) for (int64_t k = lane; k < hs; k += kWave) A.ht_global[k] = ht[k];
+    }
+    if (lane == 0) {
+        A.out_size[s] = (uint64_t)o.op;
+        if (A.status) A.status[s] = o.err;
+    }
+}
+
+template <bool PL, bool HTL, bool RING>
+__global__ __launch_bounds__(64) void k1_compress(CompressArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    for (uint64_t s = blockIdx.x; s < A.count; s += gridDim.x) {
+        compress_stream<PL, HTL, RING>(A, s, smem);
+        __syncthreads();
+    }
+}
+
+template <bool PL, bool HTL, bool RING>
+hipError_t launch_variant(const CompressArgs &a, hipStream_t st, size_t lds, unsigned grid) {
+    hipLaunchKernelGGL((k1_compress<PL, HTL, RING>), dim3(grid), dim3(64), lds, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace
+
+uint64_t compress_scratch_words(uint64_t count, int64_t hs) {
+    if (hs <= kHtLdsMax) return 0;
+    const uint64_t grid = count < 2048 ? count : 2048;
+    return grid * (uint64_t)hs;
+}
+
+hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
+    if (a.count == 0) return hipSuccess;
+    const bool htl = a.hs <= kHtLdsMax;
+    const bool pl = a.max_len > 0 && (int64_t)a.max_len <= kPLdsMax;
+    const bool ring = a.ring != nullptr;
+    size_t lds = (htl ? (size_t)a.hs * 4 : 0) + kMaskBytes + kHashBytes;
+    if (pl) lds += ((a.max_len + 3) / 4 + 8) * 4;
+    lds = (lds + 15) & ~(size_t)15;
+    uint64_t grid = a.count;
+    if (!htl && !ring) grid = grid < 2048 ? grid : 2048;  // global scratch hash tables
+    if (grid > (1u << 30)) grid = 1u << 30;
+    const unsigned g = (unsigned)grid;
+    if (pl) {
+        if (htl) return ring ? launch_variant<true, true, true>(a, st, lds, g) : launch_variant<true, true, false>(a, st, lds, g);
+        return ring ? launch_variant<true, false, true>(a, st, lds, g) : launch_variant<true, false, false>(a, st, lds, g);
+    }
+    if (htl) return ring ? launch_variant<false, true, true>(a, st, lds, g) : launch_variant<false, true, false>(a, st, lds, g);
+    return ring ? launch_variant<false, false, true>(a, st, lds, g) : launch_variant<false, false, false>(a, st, lds, g);
+}
+
+}  // namespace ez

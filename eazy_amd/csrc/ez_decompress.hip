@@ -1,0 +1,240 @@
+// ez_decompress.hip — K2: eazy decompression on gfx950.
+//
+// Restates Reader.Read's inner loop (reader.go:116-141 without more()),
+// read (:143-216), readTag (:218-270), continueMetaTag (:272-325),
+// reset (:327-344) and the Decoder (:346-514).  One wave64 per stream: the
+// token parse is wave-uniform (scalar control flow, every lane agrees); the
+// bytes of each token are produced by all 64 lanes.
+//
+// The window ring is not materialised: output is linear, so block[x & mask]
+// is the output byte at block position x (0 for x < 0: a fresh ring,
+// SURVEY A.12).  A back-reference of distance D produces
+// out[pos+k] = out[pos - D + (k mod D)], always reading bytes written by
+// earlier tokens, so every token is one hazard-free parallel pass.
+#include "ez_format.h"
+#include "ez_internal.h"
+#include "ez_wave.h"
+
+namespace ez {
+namespace {
+
+struct Dec {
+    // decoder state (reader.go:23-34)
+    int64_t bs, mask, pos, off, len;
+    int state, ver;
+    int64_t detail;
+    uint8_t *blk;  // blk[y] = byte at block position y (y >= max(0, pos - bs))
+    // input (reader.go:36-39)
+    const uint8_t *b;
+    int64_t nb, boff;
+    // config (reader.go:27-30)
+    int64_t limit;
+    bool req_magic, skip_meta;
+};
+
+// Reader.reset reader.go:327-344 (the ring is the linear output from here on)
+__device__ __forceinline__ void d_reset(Dec &d, int64_t bsl) {
+    d.bs = (int64_t)1 << bsl;
+    d.blk = d.blk + d.pos;  // next output byte is block position 0
+    d.pos = 0;
+    d.mask = d.bs - 1;
+    d.state = 0;
+}
+
+// continueMetaTag reader.go:272-325 -> err, *io = i
+__device__ int d_continue_meta(Dec &d, int64_t st, int64_t *io) {
+    int64_t i = st;
+    st--;
+    int64_t meta, l;
+    int err = dec_meta(d.b, d.nb, i, &meta, &l, &i);
+    if (err) { *io = i; return err; }
+    if (d.boff == 0 && st == 0 && meta != kMetaMagic && d.req_magic) { *io = st; return EZ_ENOMAGIC; }
+    if (i + l > d.nb) { *io = st; return EZ_ESHORTBUF; }
+    const int64_t j = meta >> 3;
+    if (j < 4) {
+        const int64_t want = j == 0 ? 4 : (j == 3 ? 0 : 1);  // tagLen {4,1,1,0}
+        if (l != want) { *io = st; return EZ_EUNSUPMETA; }
+    }
+    if (meta == kMetaMagic) {
+        if (d.b[i] != 'e' || d.b[i + 1] != 'a' || d.b[i + 2] != 'z' || d.b[i + 3] != 'y') { *io = st; return EZ_EBADMAGIC; }
+    } else if (meta == kMetaVer) {
+        d.ver = d.b[i];
+        if (d.ver > EZ_VERSION) { d.detail = d.ver; *io = st; return EZ_EUNSUPVER; }
+    } else if (meta == kMetaReset) {
+        const int64_t bsl = d.b[i];
+        if (bsl > 32 || l != 1 || (d.limit != 0 && ((int64_t)1 << bsl) > d.limit)) { *io = st; return EZ_EOVERFLOW; }
+        d_reset(d, bsl);
+    } else if (meta == kMetaBreak) {
+        *io = i + l;
+        return EZ_EBREAK;
+    } else if (!d.skip_meta) {
+        d.detail = meta;
+        *io = st;
+        return EZ_EUNSUPMETA;
+    }
+    *io = i + l;
+    return EZ_OK;
+}
+
+// readTag reader.go:218-270
+__device__ int d_read_tag(Dec &d, int64_t st, int64_t *io) {
+    int64_t i = st;
+    while (i < d.nb && d.b[i] == 0) i++;  // skip zero padding
+    st = i;
+    int tag;
+    int64_t l;
+    int err = dec_tag(d.b, d.nb, st, &tag, &l, &i);
+    if (err) { *io = st; return err; }
+    if (d.boff == 0 && st == 0 && d.b[st] != kMeta && d.req_magic) { *io = st; return EZ_ENOMAGIC; }
+    if (tag == kMeta && l == 0) return d_continue_meta(d, i, io);
+    if (d.limit != 0 && l > d.limit) { *io = st; return EZ_EBLOCKLIMIT; }
+    if (tag == kLiteral) {
+        d.state = 'l';
+        d.off = 0;
+    } else {
+        int64_t off;
+        err = dec_offset(d.b, d.nb, i, l, &off, &i);
+        if (err) { *io = st; return err; }
+        if (off > d.bs) { *io = st; return EZ_EOVERFLOW; }
+        d.off = d.pos - off;
+        d.state = 'c';
+    }
+    d.len = l;
+    *io = i;
+    return EZ_OK;
+}
+
+// Reader.read reader.go:143-216; produces at most plen bytes at blk+pos.
+// dry: compute but store nothing (capacity probe).
+__device__ int d_read(Dec &d, int64_t plen, int64_t st, int64_t *nout, int64_t *io, bool dry, int lane) {
+    int64_t i = st;
+    *nout = 0;
+    while (d.state == 0) {
+        const int err = d_read_tag(d, i, &i);
+        if (err) { *io = i; return err; }
+    }
+    if (d.bs == 0) { *io = st; return EZ_EMISSEDMETA; }
+    if (d.state == 'l' && i == d.nb) { *io = i; return EZ_ESHORTBUF; }
+    int64_t end = d.len < plen ? d.len : plen;
+    uint8_t *p = d.blk + d.pos;
+    if (d.state == 'l') {
+        const int64_t avail = d.nb - i;
+        if (end > avail) end = avail;
+        if (!dry) {
+            const uint8_t *src = d.b + i;
+            for (int64_t k = lane; k < end; k += kWave) p[k] = src[k];
+        }
+        i += end;
+    } else if (d.off == d.pos) {  // zero region (off+len <= pos is impossible here for len > 0)
+        if (!dry) for (int64_t k = lane; k < end; k += kWave) p[k] = 0;
+    } else {
+        // back-reference: non-overlapping (off+len <= pos) or runlen
+        const int64_t D = d.pos - d.off;
+        if (!dry) {
+            const uint8_t *blk = d.blk;
+            const int64_t off = d.off;
+            if (D >= end) {
+                for (int64_t k = lane; k < end; k += kWave) {
+                    const int64_t y = off + k;
+                    p[k] = y < 0 ? 0 : blk[y];
+                }
+            } else {
+                int64_t m = lane % D;
+                const int64_t step = kWave % D;
+                for (int64_t k = lane; k < end; k += kWave) {
+                    const int64_t y = off + m;
+                    p[k] = y < 0 ? 0 : blk[y];
+                    m += step;
+                    if (m >= D) m -= D;
+                }
+            }
+        }
+        d.off += end;
+    }
+    d.len -= end;
+    d.pos += end;
+    if (d.len == 0) d.state = 0;
+    *nout = end;
+    *io = i;
+    return EZ_OK;
+}
+
+// Reader.Read reader.go:116-133 minus more(): until p is full, the input
+// runs short (EZ_ESHORTBUF) or another error.
+__device__ int d_read_loop(Dec &d, int64_t plen, int64_t *i, int64_t *nout, bool dry, int lane) {
+    int64_t n = 0;
+    int err = EZ_OK;
+    while (n < plen && err == EZ_OK) {
+        int64_t m;
+        err = d_read(d, plen - n, *i, &m, i, dry, lane);
+        n += m;
+        if (n == plen) break;
+        if (err == EZ_ESHORTBUF) break;
+    }
+    *nout = n;
+    return err;
+}
+
+__global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
+    const int lane = lane_id();
+    for (uint64_t s = blockIdx.x; s < A.count; s += gridDim.x) {
+        Dec d;
+        d.b = A.in + A.in_off[s];
+        d.nb = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
+        d.limit = A.block_size_limit;
+        d.req_magic = A.require_magic != 0;
+        d.skip_meta = A.skip_unsupported_meta != 0;
+        uint8_t *out = A.out + A.out_off[s];
+        const int64_t cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+        if (A.handle) {
+            DecodeState &S = *A.st;
+            d.bs = S.bs; d.mask = S.bs ? S.bs - 1 : 0; d.pos = S.pos; d.off = S.off; d.len = S.len;
+            d.state = S.state; d.ver = S.ver; d.detail = 0; d.boff = A.boff;
+            d.blk = out - d.pos;  // the kernel's launcher keeps min(pos, bs) bytes of history before out
+            int64_t i = S.i, n = 0;
+            const int err = d_read_loop(d, cap, &i, &n, false, lane);
+            if (lane == 0) {
+                S.bs = d.bs; S.pos = d.pos; S.off = d.off; S.len = d.len; S.state = d.state; S.ver = d.ver;
+                S.i = i; S.n = n; S.detail = d.detail; S.err = err;
+                S.hist = d.bs == 0 ? 0 : (d.pos < d.bs ? d.pos : d.bs);
+            }
+            return;
+        }
+        // batch: NewReaderBytes(in) read until EOF, ErrBreak skipped
+        d.bs = 0; d.mask = 0; d.pos = 0; d.off = 0; d.len = 0; d.state = 0; d.ver = 0; d.detail = 0;
+        d.boff = 0;
+        d.blk = out;
+        int64_t i = 0, total = 0;
+        int err = EZ_OK;
+        for (int64_t guard = 0;; guard++) {
+            if (guard > d.nb + 64) { err = EZ_ESTUCK; break; }
+            const int64_t left = cap - total;
+            int64_t m;
+            if (left > 0) {
+                err = d_read_loop(d, left, &i, &m, false, lane);
+            } else {
+                err = d_read_loop(d, 1, &i, &m, true, lane);
+                if (m > 0) { err = EZ_ENOSPC; break; }
+            }
+            total += m;
+            if (err == EZ_OK || err == EZ_EBREAK) continue;
+            if (err == EZ_ESHORTBUF) err = (d.state != 0 || i < d.nb) ? EZ_EUNEXPECTEDEOF : EZ_OK;
+            break;
+        }
+        if (lane == 0) {
+            A.out_size[s] = (uint64_t)total;
+            if (A.status) A.status[s] = err;
+        }
+    }
+}
+
+}  // namespace
+
+hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
+    if (a.count == 0) return hipSuccess;
+    uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);
+    hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace ez

@@ -1,0 +1,73 @@
+// ez_internal.h — launch interface between the C-ABI (ez_capi.hip) and the
+// gfx950 kernels (ez_compress.hip, ez_decompress.hip, ez_pack.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace ez {
+
+// One K1 launch: `count` independent streams (batch) or one stream of a
+// writer handle (ring != nullptr, ht_global persistent).
+struct CompressArgs {
+    const uint8_t *in;
+    const uint64_t *in_off;   // count+1
+    uint8_t *out;
+    const uint64_t *out_off;  // count+1 (slot capacities)
+    uint64_t *out_size;       // count
+    int32_t *status;          // count or nullptr
+    uint64_t count;
+    int64_t bs;               // block (window) size, power of two
+    int64_t hs;               // hash-table entries, power of two
+    int append_magic;
+    int ver;
+    int header;               // emit the stream header first (isreset)
+    // writer-handle mode
+    int64_t start;            // stream position of in[0] (w.pos at Write entry)
+    uint8_t *ring;            // the handle's ring (block), updated in place; nullptr = fresh stream
+    uint32_t *ht_global;      // persistent hash table (handle) / per-block scratch (large hs)
+    uint64_t max_len;         // max stream length (0 = unknown)
+};
+
+// One K2 launch.  Batch: count complete streams from fresh Readers.
+// Handle: count == 1 with the streaming state in `st`.
+struct DecodeState {
+    int64_t bs;       // len(r.block) (0 = no MetaReset seen yet)
+    int64_t pos;      // r.pos
+    int64_t off;      // r.off (absolute)
+    int64_t len;      // r.len
+    int32_t state;    // 0, 'l', 'c'
+    int32_t ver;      // r.d.Ver
+    int64_t i;        // r.i (in / out)
+    int64_t n;        // bytes produced (out)
+    int64_t detail;   // meta id / version of the last error
+    int64_t hist;     // bytes of the current block held before out (handle mode)
+    int32_t err;      // result code
+    int32_t pad;
+};
+
+struct DecompressArgs {
+    const uint8_t *in;
+    const uint64_t *in_off;   // count+1
+    uint8_t *out;
+    const uint64_t *out_off;  // count+1 (capacities)
+    uint64_t *out_size;       // count
+    int32_t *status;          // count or nullptr
+    uint64_t count;
+    int64_t block_size_limit;
+    int require_magic;
+    int skip_unsupported_meta;
+    int handle;               // 1 = single streaming call (Reader.Read loop without refill)
+    int64_t boff;             // handle: absolute offset of in[0]
+    DecodeState *st;          // handle: state in/out
+};
+
+hipError_t launch_compress(const CompressArgs &a, hipStream_t s);
+// u32 words of global hash-table scratch a batch launch needs (hs too big for LDS)
+uint64_t compress_scratch_words(uint64_t count, int64_t hs);
+hipError_t launch_decompress(const DecompressArgs &a, hipStream_t s);
+hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
+                       uint8_t *packed, uint64_t *packed_off, void *workspace, hipStream_t s);
+size_t pack_workspace(uint64_t count);
+
+}  // namespace ez

@@ -1,0 +1,159 @@
+/*
+ * eazy.h — C-ABI of the MI355X-native eazy codec (libeazy_amd.so).
+ *
+ * This is the drop-in boundary a cgo shim binds (see INTEGRATION.md for the
+ * Go side).  Plain pointers and sizes only.  Every entry point names the
+ * reference (tlog-dev/eazy, Go) interface it replaces.
+ *
+ * Compute runs on AMD Instinct MI355X (gfx950) HIP kernels; there is no CPU
+ * fallback: without a usable GPU every compute entry point returns
+ * EZ_EDEVICE.  Only the scalar token codec (ez_encode_* / ez_decode_*) and
+ * ez_compress_bound are host functions; they are the reference's exported
+ * Encoder/Decoder value types, not the hot path.
+ */
+#ifndef EAZY_AMD_H
+#define EAZY_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define EZ_ABI_VERSION 1
+
+/* ---- status codes: one per reference error value (reader.go:57-76) ---- */
+enum {
+    EZ_OK = 0,
+    EZ_EOF = 1,            /* io.EOF */
+    EZ_ESHORTBUF = 2,      /* ErrShortBuffer = io.ErrShortBuffer (reader.go:62) */
+    EZ_EUNEXPECTEDEOF = 3, /* io.ErrUnexpectedEOF (reader.go:135-136) */
+    EZ_EOVERFLOW = 4,      /* ErrOverflow (reader.go:61) */
+    EZ_EBADMAGIC = 5,      /* ErrBadMagic (reader.go:58) */
+    EZ_ENOMAGIC = 6,       /* ErrNoMagic (reader.go:60) */
+    EZ_EBLOCKLIMIT = 7,    /* ErrBlockSizeOverLimit (reader.go:59) */
+    EZ_EUNSUPMETA = 8,     /* ErrUnsupportedMeta (reader.go:63, 319) */
+    EZ_EUNSUPVER = 9,      /* ErrUnsupportedVersion (reader.go:64, 303) */
+    EZ_EBREAK = 10,        /* ErrBreak (reader.go:75) */
+    EZ_EMISSEDMETA = 11,   /* errors.New("missed meta") (reader.go:155) */
+    EZ_EINVAL = 12,        /* a reference panic: bad sizes (writer.go:162-168),
+                              too big length/offset (:308-310, 562, 596), bad meta (:600-602) */
+    EZ_ESINK = 13,         /* reserved for host shims: underlying io.Writer failed */
+    EZ_ENOSPC = 14,        /* caller output buffer too small (C-ABI only) */
+    EZ_EDEVICE = 15,       /* no usable MI355X / HIP runtime error */
+    EZ_ESTUCK = 16         /* internal: a kernel's progress guard tripped */
+};
+
+/* ---- wire-format constants (writer.go:49-122) ---- */
+#define EZ_LITERAL 0x00
+#define EZ_COPY 0x80
+#define EZ_META 0x80
+#define EZ_LEN1 124
+#define EZ_LEN2 125
+#define EZ_LEN4 126
+#define EZ_LEN_ALT 127
+#define EZ_OFF1 252
+#define EZ_OFF2 253
+#define EZ_OFF4 254
+#define EZ_OFF_LONG 255
+#define EZ_META_MAGIC 0x00
+#define EZ_META_VER 0x08
+#define EZ_META_RESET 0x10
+#define EZ_META_BREAK 0x18
+#define EZ_META_LEN_WIDE 6
+#define EZ_META_LEN0 7
+#define EZ_VERSION 0
+
+const char *ez_strerror(int code);
+int ez_abi_version(void);
+/* Number of visible HIP devices (0 when none). */
+int ez_device_count(void);
+
+/* ---- low-level token codec: Encoder (writer.go:537-621), Decoder (reader.go:346-514) ----
+ * Encoders append at b[*len] (cap = total capacity of b); EZ_EINVAL where Go panics.
+ * Decoders mirror Go's (…, i, err) results: *i is `st` on any error. */
+int ez_encode_tag(uint8_t *b, size_t cap, size_t *len, int tag, int64_t l);       /* Encoder.Tag    writer.go:537 */
+int ez_encode_offset(uint8_t *b, size_t cap, size_t *len, int64_t off, int64_t l); /* Encoder.Offset writer.go:565 */
+int ez_encode_meta(uint8_t *b, size_t cap, size_t *len, int64_t meta, int64_t l);  /* Encoder.Meta   writer.go:599 */
+int ez_decode_tag(const uint8_t *b, size_t n, size_t st, int *tag, int64_t *l, size_t *i);       /* Decoder.Tag    reader.go:346 */
+int ez_decode_offset(const uint8_t *b, size_t n, size_t st, int64_t l, int64_t *off, size_t *i); /* Decoder.Offset reader.go:394 */
+int ez_decode_meta(const uint8_t *b, size_t n, size_t st, int64_t *meta, int64_t *l, size_t *i); /* Decoder.Meta   reader.go:474 */
+
+/* Upper bound of the bytes one Write of n bytes can append (header included).
+ * Derived (not in the reference); proved in tests/test_bound.py. */
+size_t ez_compress_bound(size_t n);
+
+/* ---- streaming Writer handle: the state of writer.go Writer (:17-46) ----
+ * The ring (block), hash table and stream position live in HBM on `device`.
+ * The io.Writer sink, the output buffer b, FlushThreshold and `written` stay
+ * in the host shim (writer.go:379-401); the handle tracks isreset()
+ * (writer.go:403) as "nothing emitted since the last reset". */
+typedef struct ez_writer ez_writer;
+int ez_writer_new(int64_t block, int64_t htable, int device, ez_writer **out); /* NewWriter writer.go:133 */
+void ez_writer_free(ez_writer *w);
+int ez_writer_set_append_magic(ez_writer *w, int on); /* Writer.AppendMagic writer.go:25 */
+int ez_writer_set_version(ez_writer *w, int ver);     /* Writer.e.Ver writer.go:21 */
+/* Writer.Write(p) writer.go:206-337: compresses p on the GPU and returns in
+ * out[0..*out_n) exactly the bytes Go appends to w.b for this call (header
+ * included on a pristine stream).  cap >= ez_compress_bound(n). */
+int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t *out, size_t cap, size_t *out_n);
+int ez_writer_header(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n); /* WriteHeader writer.go:342 */
+int ez_writer_break(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n);  /* WriteBreak  writer.go:358 */
+int ez_writer_reset(ez_writer *w);                                          /* Reset       writer.go:149 (reset :187) */
+int ez_writer_reset_size(ez_writer *w, int64_t block, int64_t htable);     /* ResetSize   writer.go:155 */
+int ez_writer_is_reset(const ez_writer *w);                                 /* isreset     writer.go:403 */
+
+/* ---- streaming Reader handle: the decoder state of reader.go Reader (:17-40) ----
+ * Window, position and current token live on the device.  The host shim owns
+ * r.b / r.i / r.boff and the refill from io.Reader (more(), reader.go:516-543). */
+typedef struct ez_reader ez_reader;
+int ez_reader_new(int device, ez_reader **out); /* NewReader / NewReaderBytes reader.go:79, 89 */
+void ez_reader_free(ez_reader *r);
+/* Reader.BlockSizeLimit, RequireMagic, SkipUnsupportedMeta (reader.go:27-30) */
+int ez_reader_configure(ez_reader *r, int64_t block_size_limit, int require_magic, int skip_unsupported_meta);
+int ez_reader_reset(ez_reader *r); /* the decoder part of ResetBytes reader.go:102-113 */
+/* The inner loop of Reader.Read (reader.go:119-133) without the refill:
+ * decodes from b[i..b_len) (boff = absolute offset of b[0]) into p until p is
+ * full (EZ_OK), the input runs short (EZ_ESHORTBUF: caller refills and calls
+ * again), or another error.  *n = bytes produced, *i_out = new r.i,
+ * *detail = meta id / version for EZ_EUNSUPMETA / EZ_EUNSUPVER. */
+int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size_t i, int64_t boff, uint8_t *p,
+                   size_t p_len, size_t *n, size_t *i_out, int64_t *detail);
+int ez_reader_pending(const ez_reader *r); /* r.state != 0 (reader.go:135) */
+
+/* ---- device-resident batches of independent streams (the GPU hot path) ----
+ * One stream = a fresh NewWriter(block, htable) receiving one Write; its
+ * bytes equal Go's `NewWriter(&buf, block, htable).Write(p)` output.
+ * All pointers below are DEVICE pointers on the current HIP device; calls
+ * are asynchronous on `hip_stream` (a hipStream_t, NULL = default stream). */
+typedef struct {
+    const uint8_t *in;       /* concatenated inputs */
+    const uint64_t *in_off;  /* count+1 offsets into in */
+    uint8_t *out;            /* output slots */
+    const uint64_t *out_off; /* count+1 offsets: slot s = out[out_off[s] .. out_off[s+1]) */
+    uint64_t *out_size;      /* count: bytes written into each slot */
+    int32_t *status;         /* count: EZ_* per stream (may be NULL) */
+    uint64_t count;
+    uint64_t max_len;        /* host hint: max input length of a stream (0 = unknown) */
+} ez_batch;
+
+#define EZ_F_NO_MAGIC 0x1 /* compress: AppendMagic = false */
+
+/* K1: compress every stream of b into its slot (slot >= ez_compress_bound(n)). */
+int ez_compress_batch(int64_t block, int64_t htable, int flags, const ez_batch *b, void *hip_stream);
+/* K3: exclusive scan of sizes -> packed_off[count+1], then gather the slots
+ * densely into packed.  workspace >= ez_pack_workspace(count) device bytes. */
+size_t ez_pack_workspace(uint64_t count);
+int ez_pack_batch(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
+                  uint8_t *packed, uint64_t *packed_off, void *workspace, void *hip_stream);
+/* K2: decode every compressed stream b->in[in_off[s]..in_off[s+1]) completely
+ * (NewReaderBytes + read to EOF; ErrBreak markers are skipped) into its slot.
+ * status[s] = EZ_OK on a clean end of stream, else the first error;
+ * out_size[s] = bytes produced before it. */
+int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *hip_stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* EAZY_AMD_H */

@@ -1,0 +1,125 @@
+"""GPU parity of the batched hot path (K1 compress, K3 pack, K2 decompress)
+against the CPU oracle, through the C-ABI (include/eazy.h).
+
+Bar: bit-exact compressed bytes per stream and bit-exact round trips."""
+
+import numpy as np
+import pytest
+
+import oracle as orc
+
+pytestmark = pytest.mark.gpu
+
+MiB = 1 << 20
+
+
+def _run(cuda, bufs, block=MiB, htable=1024, magic=True):
+    import torch
+
+    import eazy_amd as ez
+
+    lens = np.array([len(b) for b in bufs], np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    host = np.frombuffer(b"".join(bufs), np.uint8) if offs[-1] else np.zeros(0, np.uint8)
+    data = torch.from_numpy(host.copy()).to(cuda) if len(host) else torch.zeros(1, dtype=torch.uint8, device=cuda)
+    off = torch.from_numpy(offs).to(cuda)
+    cb = ez.compress_batch(data, off, block, htable, append_magic=magic)
+    packed, poff = ez.pack(cb)
+    out, sizes, status = ez.decompress_batch(packed, poff, off)
+    torch.cuda.synchronize()
+    return cb, packed.cpu().numpy(), poff.cpu().numpy(), out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy(), offs
+
+
+def _check(cuda, bufs, block=MiB, htable=1024, magic=True):
+    cb, pk, po, out, sizes, status, offs = _run(cuda, bufs, block, htable, magic)
+    st = cb.status.cpu().numpy()
+    for s, b in enumerate(bufs):
+        assert st[s] == 0, f"stream {s}: compress status {st[s]}"
+        want = orc.compress(block, htable, [b], append_magic=magic)
+        got = pk[po[s] : po[s + 1]].tobytes()
+        assert got == want, f"stream {s} (len {len(b)}): compressed bytes differ"
+        assert status[s] == 0, f"stream {s}: decompress status {status[s]}"
+        assert sizes[s] == len(b)
+        assert out[offs[s] : offs[s + 1]].tobytes() == b
+
+
+def test_log_batch_4k(cuda):
+    from eazy_amd import synth
+
+    d = synth.logs(3, 512 * 4096).tobytes()
+    _check(cuda, [d[k * 4096 : (k + 1) * 4096] for k in range(512)])
+
+
+def test_log_batch_64k(cuda):
+    from eazy_amd import synth
+
+    d = synth.logs(5, 8 * 65536).tobytes()
+    _check(cuda, [d[k * 65536 : (k + 1) * 65536] for k in range(8)])
+
+
+def test_ragged_and_edge_lengths(cuda):
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(11)
+    d = synth.logs(9, 1 << 20).tobytes()
+    bufs = [b"", b"a", b"ab", b"abc", b"abcd", b"aaaaaaaaaaaa", bytes(64), bytes(7), bytes(9)]
+    at = 0
+    for n in rng.integers(0, 9000, 60):
+        bufs.append(d[at : at + int(n)])
+        at += int(n)
+    _check(cuda, bufs)
+
+
+def test_small_windows_and_tables(cuda):
+    from eazy_amd import synth
+
+    d = synth.logs(13, 1 << 16).tobytes()
+    bufs = [d[k * 3000 : (k + 1) * 3000] for k in range(16)]
+    for block, htable in ((32, 16), (128, 16), (512, 32), (1024, 512), (4096, 4), (1 << 16, 1 << 13)):
+        _check(cuda, bufs, block, htable)
+
+
+def test_no_magic(cuda):
+    from eazy_amd import synth
+
+    d = synth.logs(17, 1 << 16).tobytes()
+    _check(cuda, [d[k * 4096 : (k + 1) * 4096] for k in range(16)], magic=False)
+
+
+def test_random_and_runs(cuda):
+    rng = np.random.default_rng(1)
+    bufs = []
+    for k in range(24):
+        n = int(rng.integers(100, 20000))
+        kind = k % 4
+        if kind == 0:
+            b = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        elif kind == 1:
+            b = rng.integers(0, 3, n, dtype=np.uint8).tobytes()
+        elif kind == 2:
+            b = (bytes(rng.integers(0, 256, 7, dtype=np.uint8)) * (n // 7 + 1))[:n]
+        else:
+            z = np.zeros(n, np.uint8)
+            idx = rng.integers(0, n, n // 10)
+            z[idx] = rng.integers(1, 256, len(idx), dtype=np.uint8)
+            b = z.tobytes()
+        bufs.append(b)
+    _check(cuda, bufs)
+
+
+def test_larger_than_window(cuda):
+    """Writes longer than the window exercise ring-wrap and cut (A.10)."""
+    rng = np.random.default_rng(2)
+    bufs = []
+    for block in (1024,):
+        msg = bytearray(rng.integers(0x20, 0x78, 2 * block, dtype=np.uint8).tobytes())
+        cp = b"0123456789abcdefgh"
+        msg[: len(cp)] = cp
+        msg[-len(cp) :] = cp
+        bufs.append(bytes(msg))
+        msg2 = bytearray(msg)
+        msg2[len(msg2) - block + 3 : len(msg2) - block + 3 + len(cp)] = cp
+        bufs.append(bytes(msg2))
+        bufs.append((b"abcdefgh" * 600)[:4000] + bytes(rng.integers(0, 256, 3000, dtype=np.uint8)))
+    _check(cuda, bufs, 1024, 512)
+    _check(cuda, bufs, 1024, 32)
