@@ -1,0 +1,245 @@
+"""bench.py — device-resident eazy compress+decompress throughput on MI355X.
+
+A step = one pass of the hot path over one batch resident in HBM:
+  K1 compress (writer.go Writer.Write per stream) -> K3 pack -> K2 decompress
+  (reader.go Reader.Read to EOF per stream).
+Workload at N=1 (BASELINE.json configs[1]): 65,536 independent 4 KiB
+log-like streams, NewWriter(MiB, 1024) each.  N>1: weak scaling, every rank
+owns its own 65,536-stream shard (streams are independent: no data-path
+collective).  value = uncompressed GiB processed by all ranks
+per second (GiB = 2^30 B).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       (N>1 via python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
+
+WORKLOADS = {
+    # name: (streams per GPU, bytes per stream, block, htable, description)
+    "c1": (65536, 4096, 1 << 20, 1024, "c1: 65536 x 4 KiB log-like streams per GPU, block 1 MiB, htable 1024"),
+    "c2": (4096, 256 << 10, 1 << 20, 1024, "c2: 4096 x 256 KiB log-like streams per GPU, block 1 MiB, htable 1024"),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample duration")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (rocprofv3 pass)")
+    return ap.parse_args()
+
+
+def cpu_baseline(host, offs, block, htable, seconds):
+    """The CPU restatement of the reference (oracle/, 'port') on a bounded
+    sample of the same workload, one stream per task over the box's CPU
+    share; also checks that the GPU's compressed bytes for that sample match."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle as orc
+
+    threads = max(1, min(16, os.cpu_count() or 1))
+    count = len(offs) - 1
+    chunk = min(count, 2048)
+    done_bytes, t_c, t_d, k = 0, 0.0, 0.0, 0
+    first = None
+    while (t_c + t_d) < seconds and k < count // chunk:
+        s0 = k * chunk
+        o = offs[s0 : s0 + chunk + 1] - offs[s0]
+        data = host[offs[s0] : offs[s0 + chunk]]
+        n = np.diff(o)
+        cap = n + (n >> 2) + 32
+        slot_off = np.concatenate([[0], np.cumsum(cap)]).astype(np.int64)
+        t0 = time.perf_counter()
+        slots, sizes = orc.compress_batch(block, htable, data, o.astype(np.int64), slot_off, threads)
+        t1 = time.perf_counter()
+        out, osz = orc.decompress_batch(slots, slot_off, sizes, o.astype(np.int64), threads)
+        t2 = time.perf_counter()
+        assert np.array_equal(out, data), "oracle round trip failed"
+        if first is None:
+            first = (s0, slots, slot_off, sizes)
+        t_c += t1 - t0
+        t_d += t2 - t1
+        done_bytes += int(o[-1])
+        k += 1
+    gib = done_bytes / 2**30
+    return {
+        "value": gib / (t_c + t_d),
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "compress_GiBps": gib / t_c,
+        "decompress_GiBps": gib / t_d,
+        "sample": f"{k * chunk} of the {count} streams of this rank's batch ({done_bytes / 2**20:.0f} MiB), "
+        f"C restatement of writer.go/reader.go (oracle/eazy_oracle.c, -O3), fresh NewWriter/NewReaderBytes per stream, "
+        f"{threads} host threads",
+    }, first
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    count, size, block, htable, desc = WORKLOADS[args.workload]
+    total = count * size
+    host = synth.logs(1000 + rank, total)
+    offs = synth.batch_offsets(count, size)
+    data = torch.from_numpy(host).to(dev)
+    off = torch.from_numpy(offs).to(dev)
+    slot_off = ez.slot_offsets(off)
+    cb = ez.CompressedBatch(
+        torch.empty(int(slot_off[-1]) + 16, dtype=torch.uint8, device=dev),
+        slot_off,
+        torch.empty(count, dtype=torch.int64, device=dev),
+        torch.empty(count, dtype=torch.int32, device=dev),
+    )
+    packed = torch.empty_like(cb.slots)
+    poff = torch.empty(count + 1, dtype=torch.int64, device=dev)
+    ws = torch.empty(ez._lib().ez_pack_workspace(count), dtype=torch.uint8, device=dev)
+    out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
+    osz = torch.empty(count, dtype=torch.int64, device=dev)
+    ost = torch.empty(count, dtype=torch.int32, device=dev)
+
+    def step(ev=None):
+        if ev:
+            ev[0].record()
+        ez.compress_batch(data, off, block, htable, max_len=size, out=cb)
+        if ev:
+            ev[1].record()
+        ez.pack(cb, packed, poff, ws)
+        if ev:
+            ev[2].record()
+        ez.decompress_batch(packed, poff, off, out=out, sizes=osz, status=ost)
+        if ev:
+            ev[3].record()
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    # correctness of this run: statuses, sizes and the full round trip on device
+    assert int(cb.status.abs().sum()) == 0, "compress status"
+    assert int(ost.abs().sum()) == 0, "decompress status"
+    assert bool(torch.equal(out[:total], data)), "round trip differs"
+    comp_bytes = int(poff[-1])
+
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(evs[k])
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    k1 = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
+    k3 = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
+    k2 = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
+    if world > 1:
+        t = torch.tensor([elapsed, k1, k2, k3], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, k1, k2, k3 = [float(v) for v in t.tolist()]
+        ct = torch.tensor([comp_bytes], dtype=torch.int64, device=dev)
+        dist.all_reduce(ct)
+        comp_all = int(ct.item())
+    else:
+        comp_all = comp_bytes
+
+    ms = elapsed / args.steps * 1e3
+    gib_step = total * world / 2**30
+    value = gib_step / (ms / 1e3)
+    # roofline of the dominant kernel: algorithmic bytes = input n + compressed c
+    kern = {"k1_compress": k1, "k2_decompress": k2, "k3_pack": k3}
+    dom = max(kern, key=kern.get)
+    alg = total + comp_bytes  # per launch on this rank (n + c), SURVEY.md §8d
+    achieved = alg / (kern[dom] / 1e3) / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        traffic = json.load(open(args.traffic_json)).get(dom)
+
+    res = {
+        "metric": "device-resident compress+decompress GiB/s, 1 MiB block",
+        "value": value,
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (seeded tlwire-like log events, eazy_amd/tools/synth.c)",
+        "config": {
+            "workload": desc,
+            "streams_per_gpu": count,
+            "stream_bytes": size,
+            "block": block,
+            "htable": htable,
+            "parallelism": f"dp{world} (independent stream shards, no data-path collective)",
+        },
+        "compress_GiBps": gib_step / ((k1 + k3) / 1e3),
+        "decompress_GiBps": gib_step / (k2 / 1e3),
+        "ratio": total * world / comp_all,
+        "kernel_ms": {"k1_compress": k1, "k3_pack": k3, "k2_decompress": k2},
+        "roofline": {
+            "bound": "hbm",
+            "kernel": dom,
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": alg,
+        },
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cb_res, first = cpu_baseline(host, offs, block, htable, args.cpu_seconds)
+        s0, slots, soff, sizes = first
+        g_p = packed.cpu().numpy()
+        g_o = poff.cpu().numpy()
+        for s in range(0, len(sizes), 97):  # GPU bytes == oracle bytes on the sample
+            want = slots[soff[s] : soff[s] + sizes[s]].tobytes()
+            got = g_p[g_o[s0 + s] : g_o[s0 + s + 1]].tobytes()
+            assert got == want, f"stream {s0 + s}: GPU compressed bytes differ from the oracle"
+        res["cpu_baseline"] = cb_res
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -206,8 +206,9 @@ class Writer:
         self.ver = 0
         self.b = bytearray()
         self.written = 0
-        self.sink = bytearray()
+        self._sink = bytearray()
         self.sink_writes = []
+        self.fail_accept = None
         self.block = bytearray()
         self.ht = []
         self._init(block, htable)
@@ -389,8 +390,23 @@ class Writer:
             return OK
         return self._flush()
 
-    def _flush(self):  # writer.go:387-401 (infallible sink)
-        self.sink += self.b
+    @property
+    def sink(self) -> bytes:
+        return bytes(self._sink)
+
+    def sink_fault(self, accept: int) -> None:
+        """The next sink Write takes `accept` bytes and fails."""
+        self.fail_accept = accept
+
+    def _flush(self):  # writer.go:387-401
+        if self.fail_accept is not None:
+            n = min(len(self.b), self.fail_accept)
+            self.fail_accept = None
+            self._sink += self.b[:n]
+            self.written += n
+            self._reset()
+            return ESINK
+        self._sink += self.b
         self.sink_writes.append(bytes(self.b))
         self.written += len(self.b)
         self.b = bytearray()
@@ -404,7 +420,7 @@ def compress(block: int, htable: int, writes, append_magic=True, ver=0) -> bytes
     for p in writes:
         n, err = w.write(p)
         assert err == OK and n == len(p)
-    return bytes(w.sink)
+    return w.sink
 
 
 # ---------------------------------------------------------------- Reader
@@ -435,6 +451,29 @@ class Reader:
             self.buffer_size = 64 * 1024 if buffer_size is None else buffer_size
         self.require_magic = False
         self.skip_unsupported_meta = False
+
+    def set(self, block_size_limit, buffer_size, require_magic=False, skip_unsupported_meta=False):
+        self.block_size_limit = block_size_limit
+        self.buffer_size = buffer_size
+        self.require_magic = require_magic
+        self.skip_unsupported_meta = skip_unsupported_meta
+
+    def append(self, b: bytes) -> None:
+        """More data arrives at the underlying io.Reader."""
+        self.src += b
+
+    def reset_bytes(self, b: bytes) -> None:  # ResetBytes reader.go:102-113
+        self.src = None
+        self.b = bytearray(b)
+        self.block = bytearray()
+        self.pos = 0
+        self.i = 0
+        self.boff = 0
+        self.state = 0
+
+    def reset(self, src: bytes = b"") -> None:  # Reset reader.go:96-99
+        self.reset_bytes(b"")
+        self.src = bytearray(src)
 
     def read(self, plen: int):  # Read reader.go:116-141 -> (bytes, err)
         p = bytearray(plen)

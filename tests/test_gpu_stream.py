@@ -1,0 +1,127 @@
+"""The streaming drop-in (Writer / Reader handles over the C-ABI, compute on
+the GPU) against the reference's own tests and the golden fixtures."""
+
+import numpy as np
+import pytest
+
+import impls
+import kat_suite as K
+from golden_data import h, load
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def G(cuda):
+    return impls.Gpu()
+
+
+@pytest.mark.parametrize("t", K.ALL, ids=lambda f: f.__name__)
+def test_reference_test(G, t):
+    t(G)
+
+
+def test_meta(G):
+    import eazy_amd as ez
+
+    K.t_meta(G, lambda m, l: ez.Encoder().meta(b"", m, l))
+
+
+def test_sink_failure_resets(G):
+    K.t_sink_failure_resets(G)
+
+
+def _stream(G, block, ht, writes):
+    w = G.W(block, ht)
+    for p in writes:
+        n, err = w.write(p)
+        assert err == 0 and n == len(p)
+    return w.sink
+
+
+def test_golden_fuzz_writer(G):
+    for e in load()["fuzz_writer"]:
+        writes = [h(x) for x in e["writes"]]
+        for block, ht in ((512, 32), (1 << 20, 1024)):
+            assert _stream(G, block, ht, writes).hex() == e[f"stream_{block}_{ht}"], e["name"]
+        r = G.Rb(h(e["stream_512_32"]))
+        out = bytearray()
+        while True:
+            got, err = r.read(16)
+            out += got
+            if err == 1:
+                break
+            assert err == 0
+        assert bytes(out) == b"".join(writes)
+
+
+@pytest.mark.parametrize("buf", [16, 4096])
+def test_golden_fuzz_reader(G, buf):
+    for e in load()["fuzz_reader"]:
+        r = G.Rs(h(e["input"]))
+        out, errs = bytearray(), []
+        while len(out) < (1 << 16):
+            got, err = r.read(buf)
+            out += got
+            errs.append(err)
+            if err not in (0, 10):
+                break
+        want = e[f"read{buf}"]
+        assert errs == want["errs"], e["name"]
+        assert bytes(out[: 1 << 16]).hex() == want["out"], e["name"]
+
+
+def test_golden_multi_write(G):
+    m = load()["multi_write"]
+    writes = [h(x) for x in m["writes"]]
+    assert _stream(G, 1 << 20, 1024, writes).hex() == m["stream_1048576_1024"]
+    assert _stream(G, 2048, 64, writes).hex() == m["stream_2048_64"]
+    r = G.Rb(h(m["stream_2048_64"]))
+    got, err = r.read(1 << 20)
+    assert err == 1 and got == b"".join(writes)
+
+
+def test_golden_synthetic_batch(cuda):
+    """K1/K2 batch path vs the fixtures (all three block/table configs)."""
+    import torch
+
+    import eazy_amd as ez
+
+    syn = load()["synthetic_logs"]
+    bufs = [h(e["input"]) for e in syn]
+    offs = np.concatenate([[0], np.cumsum([len(b) for b in bufs])]).astype(np.int64)
+    data = torch.from_numpy(np.frombuffer(b"".join(bufs), np.uint8).copy()).to(cuda)
+    off = torch.from_numpy(offs).to(cuda)
+    for block, ht in ((1 << 20, 1024), (1 << 17, 1024), (1024, 32)):
+        cb = ez.compress_batch(data, off, block, ht)
+        packed, poff = ez.pack(cb)
+        torch.cuda.synchronize()
+        pk, po = packed.cpu().numpy(), poff.cpu().numpy()
+        for s, e in enumerate(syn):
+            assert pk[po[s] : po[s + 1]].tobytes().hex() == e[f"stream_{block}_{ht}"]
+
+
+def test_batch_decoder_errors_match_oracle(cuda):
+    """K2 batch statuses on the FuzzReader corpus equal the oracle's
+    NewReaderBytes + read-to-EOF result (bytes and first error)."""
+    import torch
+
+    import eazy_amd as ez
+    import oracle as orc
+
+    ins = [h(e["input"]) for e in load()["fuzz_reader"]]
+    cap = 1 << 16
+    offs = np.concatenate([[0], np.cumsum([len(b) for b in ins])]).astype(np.int64)
+    comp = torch.from_numpy(np.frombuffer(b"".join(ins), np.uint8).copy()).to(cuda)
+    coff = torch.from_numpy(offs).to(cuda)
+    ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
+    out, sizes, status = ez.decompress_batch(comp, coff, ooff)
+    torch.cuda.synchronize()
+    out, sizes, status = out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy()
+    for s, b in enumerate(ins):
+        want, err, _ = orc.decompress(b, cap=cap)
+        if err == 2:  # oracle output exceeded the capacity
+            assert status[s] == ez.ENOSPC
+            continue
+        assert status[s] == err, s
+        assert out[s * cap : s * cap + sizes[s]].tobytes() == want, s
