@@ -125,6 +125,7 @@ def main():
     packed = torch.empty_like(cb.slots)
     poff = torch.empty(count + 1, dtype=torch.int64, device=dev)
     ws = torch.empty(ez._lib().ez_pack_workspace(count), dtype=torch.uint8, device=dev)
+    dws = torch.empty(ez._lib().ez_decompress_workspace(count), dtype=torch.uint8, device=dev)
     out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
     osz = torch.empty(count, dtype=torch.int64, device=dev)
     ost = torch.empty(count, dtype=torch.int32, device=dev)
@@ -138,7 +139,7 @@ def main():
         ez.pack(cb, packed, poff, ws)
         if ev:
             ev[2].record()
-        ez.decompress_batch(packed, poff, off, out=out, sizes=osz, status=ost)
+        ez.decompress_batch(packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws)
         if ev:
             ev[3].record()
 

@@ -109,7 +109,9 @@ def _lib():
     L.ez_pack_workspace.restype = sz
     L.ez_pack_workspace.argtypes = [C.c_uint64]
     L.ez_pack_batch.argtypes = [vp, vp, vp, C.c_uint64, vp, vp, vp, vp]
-    L.ez_decompress_batch.argtypes = [i64, vp, vp]
+    L.ez_decompress_workspace.restype = sz
+    L.ez_decompress_workspace.argtypes = [C.c_uint64]
+    L.ez_decompress_batch.argtypes = [i64, vp, vp, vp]
     _L = L
     return L
 
@@ -484,9 +486,10 @@ def pack(cb: CompressedBatch, packed=None, packed_off=None, workspace=None, stre
 
 
 def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=None, sizes=None, status=None,
-                     stream=None):
+                     workspace=None, exact_only: bool = False, stream=None):
     """K2: decode complete streams comp[comp_off[s]:comp_off[s+1]] into
-    out[out_off[s]:out_off[s+1]] -> (out, sizes, status)."""
+    out[out_off[s]:out_off[s+1]] -> (out, sizes, status).  exact_only skips
+    the lane-per-stream fast decoder (every stream on the exact decoder)."""
     import torch
 
     _need_cuda(comp, comp_off, out_off)
@@ -498,7 +501,10 @@ def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=Non
         sizes = torch.empty(count, dtype=torch.int64, device=dev)
     if status is None:
         status = torch.empty(count, dtype=torch.int32, device=dev)
+    if workspace is None and not exact_only:
+        workspace = torch.empty(_lib().ez_decompress_workspace(count), dtype=torch.uint8, device=dev)
     b = _Batch(comp.data_ptr(), comp_off.data_ptr(), out.data_ptr(), out_off.data_ptr(), sizes.data_ptr(),
                status.data_ptr(), count, 0)
-    _check(_lib().ez_decompress_batch(block_size_limit, C.byref(b), _stream_ptr(stream)))
+    ws = None if exact_only else workspace.data_ptr()
+    _check(_lib().ez_decompress_batch(block_size_limit, C.byref(b), ws, _stream_ptr(stream)))
     return out, sizes, status

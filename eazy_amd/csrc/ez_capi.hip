@@ -505,7 +505,11 @@ extern "C" int ez_pack_batch(const uint8_t *slots, const uint64_t *slot_off, con
     return EZ_OK;
 }
 
-extern "C" int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *hip_stream) {
+extern "C" size_t ez_decompress_workspace(uint64_t count) {
+    return (size_t)ez::decompress_workspace_words(count) * sizeof(uint32_t);
+}
+
+extern "C" int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *workspace, void *hip_stream) {
     if (device_count() <= 0) return EZ_EDEVICE;
     ez::DecompressArgs a{};
     a.in = b->in;
@@ -517,6 +521,7 @@ extern "C" int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, 
     a.count = b->count;
     a.block_size_limit = block_size_limit;
     a.handle = 0;
+    a.slow = (uint32_t *)workspace;
     EZ_HIP(ez::launch_decompress(a, (hipStream_t)hip_stream));
     return EZ_OK;
 }

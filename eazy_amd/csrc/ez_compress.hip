@@ -29,6 +29,8 @@
 #include "ez_internal.h"
 #include "ez_wave.h"
 
+#include <stdlib.h>
+
 namespace ez {
 namespace {
 
@@ -415,8 +417,20 @@ uint64_t compress_scratch_words(uint64_t count, int64_t hs) {
     return grid * (uint64_t)hs;
 }
 
+int fresh_group() {
+    static int g = -1;
+    if (g < 0) {
+        const char *e = getenv("EZ_K1_G");
+        g = e ? atoi(e) : 64;
+        if (g != 0 && g != 16 && g != 32 && g != 64) g = 64;
+    }
+    return g;
+}
+
 hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;
+    const int G = fresh_group();
+    if (G && fresh_stride_words(a, G)) return launch_compress_fresh(a, st, G);
     const bool htl = a.hs <= kHtLdsMax;
     const bool pl = a.max_len > 0 && (int64_t)a.max_len <= kPLdsMax;
     const bool ring = a.ring != nullptr;

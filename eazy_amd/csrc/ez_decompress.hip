@@ -175,9 +175,155 @@ __device__ int d_read_loop(Dec &d, int64_t plen, int64_t *i, int64_t *nout, bool
     return err;
 }
 
+
+// ---------------------------------------------------------------------------
+// K2-fast: one lane per stream (batch mode).  A lane parses its stream's
+// tokens serially and expands them with 16-byte moves; 64 streams advance in
+// parallel per wave, so the per-token parse cost is shared by 64 tokens.
+// It restates the same reader.go semantics for the common case only: header
+// metas (magic / version 0 / reset before any output), padding, breaks
+// (skipped), literal and copy tokens.  Any other condition — an error of any
+// kind, a mid-stream MetaReset, an unsupported or wide meta, a reference
+// before the stream start, a length over BlockSizeLimit, a full output slot,
+// a truncated token — hands the stream to the exact wave-per-stream decoder
+// (k2_decompress over A.slow), which recomputes it from scratch.
+
+typedef uint4 __attribute__((aligned(1))) uint4_u;
+
+__device__ __forceinline__ uint4 ld16(const uint8_t *p) { return *(const uint4_u *)p; }
+__device__ __forceinline__ void st16(uint8_t *p, uint4 v) { *(uint4_u *)p = v; }
+
+__device__ __forceinline__ uint32_t byte_of(const uint4 &w, uint32_t k) {
+    const uint32_t d = k < 8 ? (k < 4 ? w.x : w.y) : (k < 12 ? w.z : w.w);
+    return (d >> (8 * (k & 3))) & 0xff;
+}
+
+__device__ __forceinline__ uint32_t le32_at(const uint4 &w, uint32_t k) {  // 4 bytes at k (k <= 12)
+    const uint32_t a = k < 8 ? (k < 4 ? w.x : w.y) : (k < 12 ? w.z : w.w);
+    const uint32_t b = k < 8 ? (k < 4 ? w.y : w.z) : (k < 12 ? w.w : 0u);
+    return __builtin_amdgcn_alignbyte(b, a, k & 3);
+}
+
+__global__ __launch_bounds__(256) void k2_fast(DecompressArgs A) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= A.count) return;
+    const uint8_t *b = A.in + A.in_off[s];
+    const int64_t nb = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
+    const uint8_t *in_end = A.in + A.in_off[A.count];  // loads never pass the last stream's end
+    uint8_t *out = A.out + A.out_off[s];
+    const int64_t cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    const int64_t limit = A.block_size_limit;
+    int64_t i = 0, pos = 0, bs = 0;
+    bool slow = false;
+    while (i < nb) {
+        uint4 w;
+        if (b + i + 16 <= in_end) {
+            w = ld16(b + i);
+        } else {
+            uint32_t t[4] = {0, 0, 0, 0};
+            for (int k = 0; k < 16 && b + i + k < in_end; k++) t[k >> 2] |= (uint32_t)b[i + k] << (8 * (k & 3));
+            w = make_uint4(t[0], t[1], t[2], t[3]);
+        }
+        const uint32_t t0 = w.x & 0xff;
+        if (t0 == 0) { i++; continue; }  // padding (reader.go:221-224)
+        // Decoder.Tag reader.go:346-392
+        const uint32_t l7 = t0 & 0x7f;
+        int64_t L;
+        uint32_t j;
+        if (l7 < 124) { L = l7; j = 1; }
+        else if (l7 == 124) { L = 124 + byte_of(w, 1); j = 2; }
+        else if (l7 == 125) { L = 380 + (byte_of(w, 1) | byte_of(w, 2) << 8); j = 3; }
+        else if (l7 == 126) { L = 65916 + (int64_t)le32_at(w, 1); j = 5; }
+        else { slow = true; break; }  // LenAlt -> ErrOverflow
+        if (t0 & 0x80) {
+            if (L == 0) {
+                // meta (continueMetaTag reader.go:272-325)
+                if (i + 2 > nb) { slow = true; break; }
+                const uint32_t m = byte_of(w, 1);
+                const uint32_t meta = m & 0xf8, ml = m & 7;
+                int64_t ln;
+                if (ml == 7) ln = 0;
+                else if (ml < 6) ln = (int64_t)1 << ml;
+                else { slow = true; break; }  // wide meta length
+                if (i + 2 + ln > nb) { slow = true; break; }
+                if (meta == kMetaBreak && ln == 0) { i += 2; continue; }  // ErrBreak: skipped in a batch
+                if (meta == kMetaReset && ln == 1) {
+                    const uint32_t bsl = byte_of(w, 2);
+                    if (bsl > 32 || (limit != 0 && ((int64_t)1 << bsl) > limit) || pos != 0) { slow = true; break; }
+                    bs = (int64_t)1 << bsl;
+                    i += 3;
+                    continue;
+                }
+                if (meta == kMetaVer && ln == 1 && byte_of(w, 2) == 0) { i += 3; continue; }
+                if (meta == kMetaMagic && ln == 4 && le32_at(w, 2) == 0x797a6165u) { i += 6; continue; }
+                slow = true;  // anything else is an error or an unsupported meta
+                break;
+            }
+            // Decoder.Offset reader.go:394-420
+            if (limit != 0 && L > limit) { slow = true; break; }
+            uint32_t o = byte_of(w, j);
+            const bool lng = o == 0xff;
+            if (lng) { j++; o = byte_of(w, j); }
+            int64_t D;
+            if (o < 252) { D = o; j += 1; }
+            else if (o == 252) { D = 252 + byte_of(w, j + 1); j += 2; }
+            else if (o == 253) { D = 508 + (byte_of(w, j + 1) | byte_of(w, j + 2) << 8); j += 3; }
+            else if (o == 254) { D = 66044 + (int64_t)le32_at(w, j + 1); j += 5; }
+            else { slow = true; break; }  // OffAlt
+            if (!lng) D += L;
+            if (i + j > nb || bs == 0 || D > bs || D > pos || pos + L > cap) { slow = true; break; }
+            i += j;
+            uint8_t *dst = out + pos;
+            if (D == 0) {
+                // zero region (reader.go:176-179)
+                const uint4 z = make_uint4(0, 0, 0, 0);
+                int64_t k = 0;
+                for (; k + 16 <= L; k += 16) st16(dst + k, z);
+                for (; k < L; k++) dst[k] = 0;
+            } else {
+                int64_t Dd = D;
+                int64_t k = 0;
+                if (D < 16) {  // runlen: bytewise until the pattern spans >= 16 bytes
+                    Dd = D * ((16 + D - 1) / D);
+                    for (; k < L && k < Dd; k++) dst[k] = dst[k - D];
+                }
+                for (; k + 16 <= L; k += 16) st16(dst + k, ld16(dst + k - Dd));
+                if (k < L) {
+                    if (pos + k + 16 <= cap) st16(dst + k, ld16(dst + k - Dd));
+                    else for (; k < L; k++) dst[k] = dst[k - Dd];
+                }
+            }
+            pos += L;
+        } else {
+            // literal (reader.go:170-172)
+            if (limit != 0 && L > limit) { slow = true; break; }
+            if (bs == 0 || i + j + L > nb || pos + L > cap) { slow = true; break; }
+            const uint8_t *src = b + i + j;
+            uint8_t *dst = out + pos;
+            int64_t k = 0;
+            for (; k + 16 <= L; k += 16) st16(dst + k, ld16(src + k));
+            if (k < L) {
+                if (pos + k + 16 <= cap && src + k + 16 <= in_end) st16(dst + k, ld16(src + k));
+                else for (; k < L; k++) dst[k] = src[k];
+            }
+            i += j + L;
+            pos += L;
+        }
+    }
+    if (slow) {
+        const uint32_t at = atomicAdd(&A.slow[0], 1u);
+        A.slow[1 + at] = (uint32_t)s;
+    } else {
+        A.out_size[s] = (uint64_t)pos;
+        if (A.status) A.status[s] = EZ_OK;
+    }
+}
+
 __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
     const int lane = lane_id();
-    for (uint64_t s = blockIdx.x; s < A.count; s += gridDim.x) {
+    const uint64_t todo = A.slow ? (uint64_t)A.slow[0] : A.count;
+    for (uint64_t k = blockIdx.x; k < todo; k += gridDim.x) {
+        const uint64_t s = A.slow ? (uint64_t)A.slow[1 + k] : k;
         Dec d;
         d.b = A.in + A.in_off[s];
         d.nb = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
@@ -230,9 +376,20 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
 
 }  // namespace
 
+uint64_t decompress_workspace_words(uint64_t count) { return count + 16; }
+
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;
-    uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);
+    if (a.handle || !a.slow) {
+        uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+        return hipGetLastError();
+    }
+    hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k2_fast, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, st, a);
+    // exact decoder over the handed-over streams (count read on the device)
+    uint64_t grid = a.count < 4096 ? a.count : 4096;
     hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
     return hipGetLastError();
 }

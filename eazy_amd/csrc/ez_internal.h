@@ -60,9 +60,16 @@ struct DecompressArgs {
     int handle;               // 1 = single streaming call (Reader.Read loop without refill)
     int64_t boff;             // handle: absolute offset of in[0]
     DecodeState *st;          // handle: state in/out
+    uint32_t *slow;           // batch: [0] = count, [1..] = streams the fast path handed over (nullptr = exact path only)
 };
 
+// words of workspace the two-level batch decoder needs
+uint64_t decompress_workspace_words(uint64_t count);
+
 hipError_t launch_compress(const CompressArgs &a, hipStream_t s);
+// K1f: fresh streams with n <= block (ez_compress_fresh.hip); G = lanes per stream
+uint32_t fresh_stride_words(const CompressArgs &a, int G);
+hipError_t launch_compress_fresh(const CompressArgs &a, hipStream_t s, int G);
 // u32 words of global hash-table scratch a batch launch needs (hs too big for LDS)
 uint64_t compress_scratch_words(uint64_t count, int64_t hs);
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t s);

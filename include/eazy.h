@@ -150,8 +150,12 @@ int ez_pack_batch(const uint8_t *slots, const uint64_t *slot_off, const uint64_t
 /* K2: decode every compressed stream b->in[in_off[s]..in_off[s+1]) completely
  * (NewReaderBytes + read to EOF; ErrBreak markers are skipped) into its slot.
  * status[s] = EZ_OK on a clean end of stream, else the first error;
- * out_size[s] = bytes produced before it. */
-int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *hip_stream);
+ * out_size[s] = bytes produced before it (out_size is required).
+ * workspace >= ez_decompress_workspace(count) device bytes enables the
+ * lane-per-stream fast decoder (streams it cannot take are handed to the
+ * exact wave-per-stream decoder); NULL = exact decoder only. */
+size_t ez_decompress_workspace(uint64_t count);
+int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *workspace, void *hip_stream);
 
 #ifdef __cplusplus
 }

@@ -45,7 +45,7 @@ def test_no_cpu_fallback():
         ez.Reader(b=b"")
     lib = ez._lib()
     assert lib.ez_compress_batch(1 << 20, 1024, 0, None, None) == ez.EDEVICE
-    assert lib.ez_decompress_batch(0, None, None) == ez.EDEVICE
+    assert lib.ez_decompress_batch(0, None, None, None) == ez.EDEVICE
 
 
 def test_writer_size_panics():

@@ -26,7 +26,11 @@ def _run(cuda, bufs, block=MiB, htable=1024, magic=True):
     cb = ez.compress_batch(data, off, block, htable, append_magic=magic)
     packed, poff = ez.pack(cb)
     out, sizes, status = ez.decompress_batch(packed, poff, off)
+    out2, sizes2, status2 = ez.decompress_batch(packed, poff, off, exact_only=True)
     torch.cuda.synchronize()
+    # the lane-per-stream fast decoder and the exact decoder agree
+    assert torch.equal(status, status2) and torch.equal(sizes, sizes2)
+    assert torch.equal(out[: int(offs[-1])], out2[: int(offs[-1])])
     return cb, packed.cpu().numpy(), poff.cpu().numpy(), out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy(), offs
 
 

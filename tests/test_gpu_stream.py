@@ -115,9 +115,16 @@ def test_batch_decoder_errors_match_oracle(cuda):
     comp = torch.from_numpy(np.frombuffer(b"".join(ins), np.uint8).copy()).to(cuda)
     coff = torch.from_numpy(offs).to(cuda)
     ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-    out, sizes, status = ez.decompress_batch(comp, coff, ooff)
+    res = [ez.decompress_batch(comp, coff, ooff, exact_only=x) for x in (False, True)]
     torch.cuda.synchronize()
-    out, sizes, status = out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy()
+    for out, sizes, status in res:
+        _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
+
+
+def _cmp_oracle(ins, cap, out, sizes, status):
+    import eazy_amd as ez
+    import oracle as orc
+
     for s, b in enumerate(ins):
         want, err, _ = orc.decompress(b, cap=cap)
         if err == 2:  # oracle output exceeded the capacity
