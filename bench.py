@@ -41,6 +41,7 @@ def parse():
     ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stream-bytes", type=int, default=0, help="override the workload's stream size (experiments)")
     ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (rocprofv3 pass)")
     return ap.parse_args()
 
@@ -110,6 +111,9 @@ def main():
     dev = torch.device("cuda", local)
 
     count, size, block, htable, desc = WORKLOADS[args.workload]
+    if args.stream_bytes:
+        size = args.stream_bytes
+        desc += f" (stream size overridden: {size} B)"
     total = count * size
     host = synth.logs(1000 + rank, total)
     offs = synth.batch_offsets(count, size)

@@ -483,7 +483,7 @@ extern "C" int ez_compress_batch(int64_t block, int64_t htable, int flags, const
     a.start = 0;
     a.ring = nullptr;
     a.max_len = b->max_len;
-    const uint64_t words = ez::compress_scratch_words(b->count, htable);
+    const uint64_t words = ez::compress_scratch_words(a);
     if (words) {
         int dev = 0;
         EZ_HIP(hipGetDevice(&dev));

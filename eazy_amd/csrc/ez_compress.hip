@@ -411,26 +411,38 @@ hipError_t launch_variant(const CompressArgs &a, hipStream_t st, size_t lds, uns
 
 }  // namespace
 
-uint64_t compress_scratch_words(uint64_t count, int64_t hs) {
-    if (hs <= kHtLdsMax) return 0;
-    const uint64_t grid = count < 2048 ? count : 2048;
-    return grid * (uint64_t)hs;
+uint64_t compress_scratch_words(const CompressArgs &a) {
+    const char v = compress_variant(a);
+    if (v == 'l') return (lane_scratch_halves(a) + 1) / 2;
+    if (v != 'w' || a.hs <= kHtLdsMax) return 0;
+    const uint64_t grid = a.count < 2048 ? a.count : 2048;
+    return grid * (uint64_t)a.hs;
 }
 
-int fresh_group() {
-    static int g = -1;
-    if (g < 0) {
-        const char *e = getenv("EZ_K1_G");
-        g = e ? atoi(e) : 64;
-        if (g != 0 && g != 16 && g != 32 && g != 64) g = 64;
+// K1 variant choice: EZ_K1=lane|g16|wave|general overrides (A/B measurement)
+char compress_variant(const CompressArgs &a) {
+    static int forced = -1;
+    if (forced < 0) {
+        const char *e = getenv("EZ_K1");
+        forced = !e ? 0 : (e[0] == 'l' ? 'l' : e[0] == 'g' && e[1] == '1' ? 'g' : e[0] == 'w' ? 'f' : e[0] == 'g' ? 'w' : 0);
     }
-    return g;
+    const bool lane = lane_scratch_halves(a) != 0, g16 = g16_stride_words(a) != 0, fresh = fresh_stride_words(a, 64) != 0;
+    if (forced == 'l' && lane) return 'l';
+    if (forced == 'g' && g16) return 'g';
+    if (forced == 'f' && fresh) return 'f';
+    if (forced == 'w') return 'w';
+    if (lane && a.count >= 16384) return 'l';  // enough streams to fill the chip one lane each
+    if (g16) return 'g';
+    if (fresh) return 'f';
+    return 'w';
 }
 
 hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;
-    const int G = fresh_group();
-    if (G && fresh_stride_words(a, G)) return launch_compress_fresh(a, st, G);
+    const char v = compress_variant(a);
+    if (v == 'l') return launch_compress_lane(a, (uint16_t *)a.ht_global, st);
+    if (v == 'g') return launch_compress_g16(a, st);
+    if (v == 'f') return launch_compress_fresh(a, st, 64);
     const bool htl = a.hs <= kHtLdsMax;
     const bool pl = a.max_len > 0 && (int64_t)a.max_len <= kPLdsMax;
     const bool ring = a.ring != nullptr;

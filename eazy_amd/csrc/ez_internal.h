@@ -70,8 +70,16 @@ hipError_t launch_compress(const CompressArgs &a, hipStream_t s);
 // K1f: fresh streams with n <= block (ez_compress_fresh.hip); G = lanes per stream
 uint32_t fresh_stride_words(const CompressArgs &a, int G);
 hipError_t launch_compress_fresh(const CompressArgs &a, hipStream_t s, int G);
+// K1l: fresh streams, one lane per stream (ez_compress_lane.hip); u16 scratch count*hs
+uint64_t lane_scratch_halves(const CompressArgs &a);
+hipError_t launch_compress_lane(const CompressArgs &a, uint16_t *scratch, hipStream_t s);
+// the K1 variant a batch launch takes: 'l' lane, 'g' g16, 'f' fresh wave, 'w' general wave
+char compress_variant(const CompressArgs &a);
+// K1g: fresh streams, 16 lanes per stream (ez_compress_g16.hip)
+uint32_t g16_stride_words(const CompressArgs &a);
+hipError_t launch_compress_g16(const CompressArgs &a, hipStream_t s);
 // u32 words of global hash-table scratch a batch launch needs (hs too big for LDS)
-uint64_t compress_scratch_words(uint64_t count, int64_t hs);
+uint64_t compress_scratch_words(const CompressArgs &a);
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t s);
 hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
                        uint8_t *packed, uint64_t *packed_off, void *workspace, hipStream_t s);
