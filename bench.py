@@ -42,6 +42,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--stream-bytes", type=int, default=0, help="override the workload's stream size (experiments)")
+    ap.add_argument("--no-check", action="store_true", help="skip the round-trip checks (timing experiments only)")
+    ap.add_argument("--streams", type=int, default=0, help="override the workload's stream count (experiments)")
     ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (rocprofv3 pass)")
     return ap.parse_args()
 
@@ -114,6 +116,9 @@ def main():
     if args.stream_bytes:
         size = args.stream_bytes
         desc += f" (stream size overridden: {size} B)"
+    if args.streams:
+        count = args.streams
+        desc += f" (stream count overridden: {count})"
     total = count * size
     host = synth.logs(1000 + rank, total)
     offs = synth.batch_offsets(count, size)
@@ -151,9 +156,10 @@ def main():
         step()
     torch.cuda.synchronize()
     # correctness of this run: statuses, sizes and the full round trip on device
-    assert int(cb.status.abs().sum()) == 0, "compress status"
-    assert int(ost.abs().sum()) == 0, "decompress status"
-    assert bool(torch.equal(out[:total], data)), "round trip differs"
+    if not args.no_check:
+        assert int(cb.status.abs().sum()) == 0, "compress status"
+        assert int(ost.abs().sum()) == 0, "decompress status"
+        assert bool(torch.equal(out[:total], data)), "round trip differs"
     comp_bytes = int(poff[-1])
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]

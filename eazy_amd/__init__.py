@@ -23,7 +23,7 @@ import os
 from dataclasses import dataclass
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libeazy_amd.so")
+LIB_PATH = os.environ.get("EZ_LIB") or os.path.join(_HERE, "libeazy_amd.so")  # EZ_LIB: experiment builds
 
 # ---- constants (writer.go:49-122) ----
 B, KiB, MiB, GiB = 1, 1 << 10, 1 << 20, 1 << 30

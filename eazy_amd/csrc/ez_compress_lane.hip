@@ -318,8 +318,9 @@ uint64_t lane_scratch_halves(const CompressArgs &a) {
 }
 
 hipError_t launch_compress_lane(const CompressArgs &a, uint16_t *scratch, hipStream_t st) {
-    const unsigned grid = (unsigned)((a.count + 255) / 256);
-    hipLaunchKernelGGL(k1_lane, dim3(grid), dim3(256), 0, st, a, scratch);
+    static const unsigned blk = getenv("EZ_K1_BLOCK") ? (unsigned)atoi(getenv("EZ_K1_BLOCK")) : 256u;
+    const unsigned grid = (unsigned)((a.count + blk - 1) / blk);
+    hipLaunchKernelGGL(k1_lane, dim3(grid), dim3(blk), 0, st, a, scratch);
     return hipGetLastError();
 }
 

@@ -189,127 +189,242 @@ __device__ int d_read_loop(Dec &d, int64_t plen, int64_t *i, int64_t *nout, bool
 // (k2_decompress over A.slow), which recomputes it from scratch.
 
 typedef uint4 __attribute__((aligned(1))) uint4_u;
+typedef unsigned __int128 u128;
 
+__device__ __forceinline__ u128 to128(uint4 v) {
+    return ((u128)((uint64_t)v.z | ((uint64_t)v.w << 32)) << 64) | ((uint64_t)v.x | ((uint64_t)v.y << 32));
+}
+__device__ __forceinline__ uint4 from128(u128 x) {
+    const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
+    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+}
 __device__ __forceinline__ uint4 ld16(const uint8_t *p) { return *(const uint4_u *)p; }
 __device__ __forceinline__ void st16(uint8_t *p, uint4 v) { *(uint4_u *)p = v; }
+__device__ __forceinline__ uint32_t bat(u128 h, uint32_t k) { return (uint32_t)(h >> (8 * k)) & 0xff; }
+__device__ __forceinline__ uint32_t le32at(u128 h, uint32_t k) { return (uint32_t)(h >> (8 * k)); }
 
-__device__ __forceinline__ uint32_t byte_of(const uint4 &w, uint32_t k) {
-    const uint32_t d = k < 8 ? (k < 4 ? w.x : w.y) : (k < 12 ? w.z : w.w);
-    return (d >> (8 * (k & 3))) & 0xff;
+// 16 input bytes at q (q < end), never reading at or past `end` (bytes there
+// read as 0): one clamped load shifted into place.  The launcher routes
+// batches under 16 input bytes to the exact decoder.
+__device__ __forceinline__ u128 ld_in(const uint8_t *q, const uint8_t *end) {
+    const int64_t over = (q + 16) - end;
+    if (over <= 0) return to128(ld16(q));
+    const u128 x = to128(ld16(end - 16));
+    return over >= 16 ? (u128)0 : x >> (8 * over);
 }
 
-__device__ __forceinline__ uint32_t le32_at(const uint4 &w, uint32_t k) {  // 4 bytes at k (k <= 12)
-    const uint32_t a = k < 8 ? (k < 4 ? w.x : w.y) : (k < 12 ? w.z : w.w);
-    const uint32_t b = k < 8 ? (k < 4 ? w.y : w.z) : (k < 12 ? w.w : 0u);
-    return __builtin_amdgcn_alignbyte(b, a, k & 3);
+// 16 bytes of a stream's output history at y (y < dst): bytes before the
+// slot start read as 0 (the decoder's fresh window, reader.go:176-196).
+// Needs a slot of at least 16 bytes when y < 0.
+__device__ __forceinline__ u128 ld_hist(const uint8_t *out, int64_t y) {
+    if (y >= 0) return to128(ld16(out + y));
+    if (y <= -16) return 0;
+    return to128(ld16(out)) << (8 * -y);
+}
+
+// k < 16 bytes of x at d: 8/4/2/1-byte stores, no loop
+__device__ __forceinline__ void put_small(uint8_t *d, u128 x, int64_t k) {
+    typedef uint64_t __attribute__((aligned(1))) u64_u;
+    typedef uint32_t __attribute__((aligned(1))) u32_u;
+    typedef uint16_t __attribute__((aligned(1))) u16_u;
+    int64_t o = 0;
+    if (k & 8) { *(u64_u *)(d + o) = (uint64_t)x; x >>= 64; o += 8; }
+    if (k & 4) { *(u32_u *)(d + o) = (uint32_t)x; x >>= 32; o += 4; }
+    if (k & 2) { *(u16_u *)(d + o) = (uint16_t)x; x >>= 16; o += 2; }
+    if (k & 1) d[o] = (uint8_t)x;
+}
+
+// One iteration = (parse the next token from registers when the previous one
+// is written) + (one 16-byte move).  All loads of an iteration — the move's
+// source and the prefetch of the next 16 compressed bytes — are issued
+// together, so a lane waits for memory once per iteration.
+#ifndef EZ_EXP
+#define EZ_EXP 0  // timing experiments only (1: no stores, 2: no data loads, 3: neither)
+#endif
+enum : int { M_REG = 0, M_IN = 1, M_OUT = 2, M_PAT = 3, M_PATLD = 4 };
+
+// the low `per` bytes of x (1 <= per < 16) repeated over 16 bytes
+__device__ __forceinline__ u128 run_pattern(u128 x, int32_t per) {
+    x &= ((u128)1 << (8 * per)) - 1;
+    x |= x << (8 * per);
+    if (2 * per < 16) x |= x << (16 * per);
+    if (4 * per < 16) x |= x << (32 * per);
+    if (8 * per < 16) x |= x << (64 * per);
+    return x;
 }
 
 __global__ __launch_bounds__(256) void k2_fast(DecompressArgs A) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= A.count) return;
     const uint8_t *b = A.in + A.in_off[s];
-    const int64_t nb = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
+    int64_t nb = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
     const uint8_t *in_end = A.in + A.in_off[A.count];  // loads never pass the last stream's end
     uint8_t *out = A.out + A.out_off[s];
     const int64_t cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
     const int64_t limit = A.block_size_limit;
     int64_t i = 0, pos = 0, bs = 0;
-    bool slow = false;
-    while (i < nb) {
-        uint4 w;
-        if (b + i + 16 <= in_end) {
-            w = ld16(b + i);
-        } else {
-            uint32_t t[4] = {0, 0, 0, 0};
-            for (int k = 0; k < 16 && b + i + k < in_end; k++) t[k >> 2] |= (uint32_t)b[i + k] << (8 * (k & 3));
-            w = make_uint4(t[0], t[1], t[2], t[3]);
-        }
-        const uint32_t t0 = w.x & 0xff;
-        if (t0 == 0) { i++; continue; }  // padding (reader.go:221-224)
-        // Decoder.Tag reader.go:346-392
-        const uint32_t l7 = t0 & 0x7f;
-        int64_t L;
-        uint32_t j;
-        if (l7 < 124) { L = l7; j = 1; }
-        else if (l7 == 124) { L = 124 + byte_of(w, 1); j = 2; }
-        else if (l7 == 125) { L = 380 + (byte_of(w, 1) | byte_of(w, 2) << 8); j = 3; }
-        else if (l7 == 126) { L = 65916 + (int64_t)le32_at(w, 1); j = 5; }
-        else { slow = true; break; }  // LenAlt -> ErrOverflow
-        if (t0 & 0x80) {
-            if (L == 0) {
-                // meta (continueMetaTag reader.go:272-325)
-                if (i + 2 > nb) { slow = true; break; }
-                const uint32_t m = byte_of(w, 1);
-                const uint32_t meta = m & 0xf8, ml = m & 7;
-                int64_t ln;
-                if (ml == 7) ln = 0;
-                else if (ml < 6) ln = (int64_t)1 << ml;
-                else { slow = true; break; }  // wide meta length
-                if (i + 2 + ln > nb) { slow = true; break; }
-                if (meta == kMetaBreak && ln == 0) { i += 2; continue; }  // ErrBreak: skipped in a batch
-                if (meta == kMetaReset && ln == 1) {
-                    const uint32_t bsl = byte_of(w, 2);
-                    if (bsl > 32 || (limit != 0 && ((int64_t)1 << bsl) > limit) || pos != 0) { slow = true; break; }
-                    bs = (int64_t)1 << bsl;
-                    i += 3;
-                    continue;
-                }
-                if (meta == kMetaVer && ln == 1 && byte_of(w, 2) == 0) { i += 3; continue; }
-                if (meta == kMetaMagic && ln == 4 && le32_at(w, 2) == 0x797a6165u) { i += 6; continue; }
-                slow = true;  // anything else is an error or an unsupported meta
-                break;
-            }
-            // Decoder.Offset reader.go:394-420
-            if (limit != 0 && L > limit) { slow = true; break; }
-            uint32_t o = byte_of(w, j);
-            const bool lng = o == 0xff;
-            if (lng) { j++; o = byte_of(w, j); }
-            int64_t D;
-            if (o < 252) { D = o; j += 1; }
-            else if (o == 252) { D = 252 + byte_of(w, j + 1); j += 2; }
-            else if (o == 253) { D = 508 + (byte_of(w, j + 1) | byte_of(w, j + 2) << 8); j += 3; }
-            else if (o == 254) { D = 66044 + (int64_t)le32_at(w, j + 1); j += 5; }
-            else { slow = true; break; }  // OffAlt
-            if (!lng) D += L;
-            if (i + j > nb || bs == 0 || D > bs || D > pos || pos + L > cap) { slow = true; break; }
-            i += j;
-            uint8_t *dst = out + pos;
-            if (D == 0) {
-                // zero region (reader.go:176-179)
-                const uint4 z = make_uint4(0, 0, 0, 0);
-                int64_t k = 0;
-                for (; k + 16 <= L; k += 16) st16(dst + k, z);
-                for (; k < L; k++) dst[k] = 0;
+    bool slow = in_end - A.in < 16;  // ld_in's clamped loads need 16 input bytes
+    // register window over the compressed stream: bytes [wb, wb + 32); i - wb < 16 at a parse
+    int64_t wb = 0;
+    u128 c0 = 0, c1 = 0;
+    if (!slow) {
+        c0 = ld_in(b, in_end);
+        c1 = ld_in(b + 16, in_end);
+    } else {
+        nb = 0;  // skip the loop: the exact decoder takes the stream
+    }
+    // the token being written: rem bytes at out + dst, from src (input or output offset)
+    int64_t rem = 0, dst = 0, src = 0, Dd = 16;
+    int32_t per = 0;
+    int mode = M_REG;
+#if EZ_EXP == 1 || EZ_EXP == 3
+    u128 sinkv = 0;
+#endif
+    u128 v = 0;
+    for (;;) {
+        if (rem == 0) {
+            if (i >= nb) break;
+            const int64_t r = i - wb;
+            const u128 h = r ? (c0 >> (8 * r)) | (c1 << (128 - 8 * r)) : c0;  // bytes i .. i+15
+            const uint32_t t0 = (uint32_t)h & 0xff;
+            if (t0 == 0) {  // padding (reader.go:221-224), a run of zero bytes at once
+                const uint64_t lo = (uint64_t)h, hi = (uint64_t)(h >> 64);
+                i += lo ? (__builtin_ctzll(lo) >> 3) : (hi ? 8 + (__builtin_ctzll(hi) >> 3) : 16);
             } else {
-                int64_t Dd = D;
-                int64_t k = 0;
-                if (D < 16) {  // runlen: bytewise until the pattern spans >= 16 bytes
-                    Dd = D * ((16 + D - 1) / D);
-                    for (; k < L && k < Dd; k++) dst[k] = dst[k - D];
-                }
-                for (; k + 16 <= L; k += 16) st16(dst + k, ld16(dst + k - Dd));
-                if (k < L) {
-                    if (pos + k + 16 <= cap) st16(dst + k, ld16(dst + k - Dd));
-                    else for (; k < L; k++) dst[k] = dst[k - Dd];
+                // Decoder.Tag reader.go:346-392
+                const uint32_t l7 = t0 & 0x7f;
+                int64_t L;
+                uint32_t j;
+                if (l7 < 124) { L = l7; j = 1; }
+                else if (l7 == 124) { L = 124 + bat(h, 1); j = 2; }
+                else if (l7 == 125) { L = 380 + (le32at(h, 1) & 0xffff); j = 3; }
+                else if (l7 == 126) { L = 65916 + (int64_t)le32at(h, 1); j = 5; }
+                else { slow = true; break; }  // LenAlt -> ErrOverflow
+                if (t0 & 0x80) {
+                    if (L == 0) {
+                        // meta (continueMetaTag reader.go:272-325)
+                        if (i + 2 > nb) { slow = true; break; }
+                        const uint32_t m = bat(h, 1);
+                        const uint32_t meta = m & 0xf8, ml = m & 7;
+                        int64_t ln;
+                        if (ml == 7) ln = 0;
+                        else if (ml < 6) ln = (int64_t)1 << ml;
+                        else { slow = true; break; }  // wide meta length
+                        if (i + 2 + ln > nb) { slow = true; break; }
+                        if (meta == kMetaBreak && ln == 0) {
+                            i += 2;  // ErrBreak: skipped in a batch
+                        } else if (meta == kMetaReset && ln == 1) {
+                            const uint32_t bsl = bat(h, 2);
+                            if (bsl > 32 || (limit != 0 && ((int64_t)1 << bsl) > limit) || pos != 0) { slow = true; break; }
+                            bs = (int64_t)1 << bsl;
+                            i += 3;
+                        } else if (meta == kMetaVer && ln == 1 && bat(h, 2) == 0) {
+                            i += 3;
+                        } else if (meta == kMetaMagic && ln == 4 && le32at(h, 2) == 0x797a6165u) {
+                            i += 6;
+                        } else {
+                            slow = true;  // an error or an unsupported meta
+                            break;
+                        }
+                    } else {
+                        // Decoder.Offset reader.go:394-420
+                        if (limit != 0 && L > limit) { slow = true; break; }
+                        uint32_t o = bat(h, j);
+                        const bool lng = o == 0xff;
+                        if (lng) { j++; o = bat(h, j); }
+                        int64_t D;
+                        if (o < 252) { D = o; j += 1; }
+                        else if (o == 252) { D = 252 + bat(h, j + 1); j += 2; }
+                        else if (o == 253) { D = 508 + (le32at(h, j + 1) & 0xffff); j += 3; }
+                        else if (o == 254) { D = 66044 + (int64_t)le32at(h, j + 1); j += 5; }
+                        else { slow = true; break; }  // OffAlt
+                        if (!lng) D += L;
+                        if (i + j > nb || bs == 0 || D > bs || pos + L > cap || (D > pos && cap < 16)) { slow = true; break; }
+                        i += j;
+                        dst = pos;
+                        rem = L;
+                        pos += L;
+                        Dd = 16;
+                        if (D == 0) {  // zero region (reader.go:176-179)
+                            mode = M_REG;
+                            v = 0;
+                        } else if (D < 16) {  // short-period run: a 16-byte pattern every Dd bytes
+                            Dd = D * (16 / D);
+                            per = (int32_t)D;
+                            mode = M_PATLD;
+                            src = dst - 16;
+                        } else {
+                            mode = M_OUT;
+                            src = dst - D;
+                        }
+                    }
+                } else {
+                    // literal (reader.go:170-172)
+                    if (limit != 0 && L > limit) { slow = true; break; }
+                    if (bs == 0 || i + j + L > nb || pos + L > cap) { slow = true; break; }
+                    dst = pos;
+                    rem = L;
+                    pos += L;
+                    Dd = 16;
+                    if (j + L <= 16) {  // bytes straight from the header window
+                        mode = M_REG;
+                        v = h >> (8 * j);
+                    } else {
+                        mode = M_IN;
+                        src = i + j;
+                    }
+                    i += j + L;
                 }
             }
-            pos += L;
-        } else {
-            // literal (reader.go:170-172)
-            if (limit != 0 && L > limit) { slow = true; break; }
-            if (bs == 0 || i + j + L > nb || pos + L > cap) { slow = true; break; }
-            const uint8_t *src = b + i + j;
-            uint8_t *dst = out + pos;
-            int64_t k = 0;
-            for (; k + 16 <= L; k += 16) st16(dst + k, ld16(src + k));
-            if (k < L) {
-                if (pos + k + 16 <= cap && src + k + 16 <= in_end) st16(dst + k, ld16(src + k));
-                else for (; k < L; k++) dst[k] = src[k];
+        }
+        // ---- loads of this iteration, issued together ----
+        u128 raw = 0;
+#if EZ_EXP != 2 && EZ_EXP != 3
+        if (rem > 0 && (mode == M_IN || mode == M_OUT || mode == M_PATLD))
+            raw = mode == M_IN ? ld_in(b + src, in_end) : ld_hist(out, src);
+#else
+        raw = c0 ^ (u128)src;
+#endif
+        const bool rebase = i - wb >= 32;
+        u128 n0 = 0, n1 = 0;
+        if (rebase) {
+            n0 = ld_in(b + i, in_end);
+            n1 = ld_in(b + i + 16, in_end);
+        } else if (i - wb >= 16) {
+            n1 = ld_in(b + wb + 32, in_end);
+        }
+        // ---- the move ----
+        if (rem > 0) {
+            if (mode == M_PATLD) {  // raw = the 16 bytes before dst; the period is its top `per` bytes
+                v = run_pattern(raw >> (8 * (16 - per)), per);
+                mode = M_PAT;
+            } else if (mode != M_REG && mode != M_PAT) {
+                v = raw;
             }
-            i += j + L;
-            pos += L;
+#if EZ_EXP != 1 && EZ_EXP != 3
+            if (rem >= 16 || dst + 16 <= cap) st16(out + dst, from128(v));
+            else put_small(out + dst, v, rem);
+#else
+            sinkv ^= v;
+#endif
+            const int64_t step = rem < Dd ? rem : Dd;
+            dst += step;
+            src += step;
+            rem -= step;
+        }
+        if (rebase) {
+            wb = i;
+            c0 = n0;
+            c1 = n1;
+        } else if (i - wb >= 16) {
+            wb += 16;
+            c0 = c1;
+            c1 = n1;
         }
     }
+#if EZ_EXP == 1 || EZ_EXP == 3
+    if ((uint64_t)sinkv == 0x123456789ull) pos++;
+#endif
     if (slow) {
         const uint32_t at = atomicAdd(&A.slow[0], 1u);
         A.slow[1 + at] = (uint32_t)s;
@@ -387,7 +502,8 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     }
     hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k2_fast, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, st, a);
+    static const unsigned blk = getenv("EZ_K2_BLOCK") ? (unsigned)atoi(getenv("EZ_K2_BLOCK")) : 256u;
+    hipLaunchKernelGGL(k2_fast, dim3((unsigned)((a.count + blk - 1) / blk)), dim3(blk), 0, st, a);
     // exact decoder over the handed-over streams (count read on the device)
     uint64_t grid = a.count < 4096 ? a.count : 4096;
     hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
