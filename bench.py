@@ -104,9 +104,10 @@ def main():
     import eazy_amd as ez
     from eazy_amd import synth
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from eazy_amd import dist as ezd
+
+    R = ezd.from_env()
+    world, rank, local = R.world, R.rank, R.local
     if world > 1:
         dist.init_process_group("nccl")
     torch.cuda.set_device(local)
@@ -120,7 +121,7 @@ def main():
         count = args.streams
         desc += f" (stream count overridden: {count})"
     total = count * size
-    host = synth.logs(1000 + rank, total)
+    host = synth.logs(ezd.seed(1000, R), total)  # this rank's shard of independent streams
     offs = synth.batch_offsets(count, size)
     data = torch.from_numpy(host).to(dev)
     off = torch.from_numpy(offs).to(dev)
@@ -163,29 +164,20 @@ def main():
     comp_bytes = int(poff[-1])
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
+    ezd.barrier(R)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
         step(evs[k])
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
+    ezd.barrier(R)
     elapsed = t1 - t0
     k1 = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     k3 = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     k2 = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
-    if world > 1:
-        t = torch.tensor([elapsed, k1, k2, k3], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, k1, k2, k3 = [float(v) for v in t.tolist()]
-        ct = torch.tensor([comp_bytes], dtype=torch.int64, device=dev)
-        dist.all_reduce(ct)
-        comp_all = int(ct.item())
-    else:
-        comp_all = comp_bytes
+    elapsed, k1, k2, k3 = ezd.reduce_max([elapsed, k1, k2, k3], R, dev)  # the job ends with its slowest rank
+    (comp_all,) = ezd.reduce_sum([comp_bytes], R, dev)
 
     ms = elapsed / args.steps * 1e3
     gib_step = total * world / 2**30

@@ -1,0 +1,349 @@
+// eazy.hpp — C++ host side of the MI355X eazy codec, over the C-ABI of
+// include/eazy.h (libeazy_amd.so).
+//
+// It mirrors the reference Go package's exported surface (tlog-dev/eazy):
+// the same names, argument meaning and error behaviour, so C++ callers and
+// the parity tests (tests/cpp/eazy_test.cpp) read like eazy_test.go.
+//
+//   Go (reference)                               C++ (here)
+//   NewWriter(w io.Writer, block, htable int)    eazy::NewWriter(IoWriter*, block, htable)   writer.go:133
+//   (*Writer).Write(p) (int, error)              Writer::Write(p, n) -> {n, Err}             writer.go:206
+//   WriteHeader / WriteBreak / Flush             Writer::WriteHeader / WriteBreak / Flush    writer.go:342-377
+//   Reset(w) / ResetSize(w, block, htable)       Writer::Reset / ResetSize                   writer.go:149-159
+//   Writer.AppendMagic / FlushThreshold          Writer::AppendMagic / FlushThreshold        writer.go:23-34
+//   NewReader(r io.Reader) / NewReaderBytes(b)   eazy::NewReader / NewReaderBytes            reader.go:79, 89
+//   (*Reader).Read(p) (int, error)               Reader::Read(p, n) -> {n, Err}              reader.go:116
+//   Reset(r) / ResetBytes(b)                     Reader::Reset / ResetBytes                  reader.go:96-113
+//   BlockSizeLimit, BufferSize, RequireMagic,    same public fields                          reader.go:27-30
+//   SkipUnsupportedMeta
+//   Encoder{Ver}.Tag/Offset/Meta                 eazy::Encoder                               writer.go:537-621
+//   Decoder{Ver}.Tag/Offset/Meta                 eazy::Decoder                               reader.go:346-514
+//   error values ErrOverflow, ErrBreak, ...      eazy::Err (one code per value)              reader.go:57-76
+//   panics (bad sizes, impossible lengths)       eazy::Panic exception                        writer.go:162-168
+//
+// The compute (Writer.Write's match-find/emit, Reader.Read's decode) runs in
+// the HIP kernels behind the C-ABI; with no usable GPU those calls fail with
+// Err::Device (there is no CPU fallback).  The io.Writer / io.Reader plumbing,
+// the output buffer, FlushThreshold and the input refill (more()) live here,
+// exactly where the reference keeps them (writer.go:379-401, reader.go:516-543).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../../include/eazy.h"
+
+namespace eazy {
+
+constexpr int64_t KiB = 1 << 10;
+constexpr int64_t MiB = 1 << 20;
+
+// Token and meta constants (writer.go:49-122)
+constexpr int Literal = EZ_LITERAL, Copy = EZ_COPY, Meta = EZ_META;
+constexpr int Len1 = EZ_LEN1, Len2 = EZ_LEN2, Len4 = EZ_LEN4, LenAlt = EZ_LEN_ALT;
+constexpr int Off1 = EZ_OFF1, Off2 = EZ_OFF2, Off4 = EZ_OFF4, OffLong = EZ_OFF_LONG;
+constexpr int MetaMagic = EZ_META_MAGIC, MetaVer = EZ_META_VER, MetaReset = EZ_META_RESET, MetaBreak = EZ_META_BREAK;
+constexpr int MetaLenWide = EZ_META_LEN_WIDE, MetaLen0 = EZ_META_LEN0, MetaTagMask = 0xf8;
+constexpr const char Magic[] = "eazy";
+
+// One code per reference error value (reader.go:57-76) plus the C-ABI's own.
+enum class Err : int {
+    OK = EZ_OK,
+    EOF_ = EZ_EOF,                        // io.EOF
+    ShortBuffer = EZ_ESHORTBUF,           // ErrShortBuffer
+    UnexpectedEOF = EZ_EUNEXPECTEDEOF,    // io.ErrUnexpectedEOF
+    Overflow = EZ_EOVERFLOW,              // ErrOverflow
+    BadMagic = EZ_EBADMAGIC,              // ErrBadMagic
+    NoMagic = EZ_ENOMAGIC,                // ErrNoMagic
+    BlockSizeOverLimit = EZ_EBLOCKLIMIT,  // ErrBlockSizeOverLimit
+    UnsupportedMeta = EZ_EUNSUPMETA,      // ErrUnsupportedMeta
+    UnsupportedVersion = EZ_EUNSUPVER,    // ErrUnsupportedVersion
+    Break = EZ_EBREAK,                    // ErrBreak
+    MissedMeta = EZ_EMISSEDMETA,          // "missed meta"
+    Invalid = EZ_EINVAL,                  // a Go panic (thrown as Panic by this header)
+    Sink = EZ_ESINK,                      // the io.Writer failed
+    NoSpace = EZ_ENOSPC,
+    Device = EZ_EDEVICE,                  // no usable MI355X
+    Stuck = EZ_ESTUCK,
+};
+
+inline const char *ErrString(Err e) { return ez_strerror((int)e); }
+
+// What Go does with panic(): invalid sizes, impossible lengths, bad meta.
+struct Panic : std::logic_error {
+    explicit Panic(const std::string &w) : std::logic_error(w) {}
+};
+
+// io.Writer: returns bytes taken and an error (Err::OK on success).
+struct IoWriter {
+    virtual ~IoWriter() = default;
+    virtual std::pair<size_t, Err> Write(const uint8_t *p, size_t n) = 0;
+};
+
+// io.Reader with Go semantics: may return n > 0 together with Err::EOF_.
+struct IoReader {
+    virtual ~IoReader() = default;
+    virtual std::pair<size_t, Err> Read(uint8_t *p, size_t n) = 0;
+};
+
+// bytes.Buffer-like in-memory sink/source (the reference tests' low.Buf / bytes.Buffer)
+struct Buffer : IoWriter, IoReader {
+    std::vector<uint8_t> b;
+    size_t r = 0;
+    std::pair<size_t, Err> Write(const uint8_t *p, size_t n) override {
+        b.insert(b.end(), p, p + n);
+        return {n, Err::OK};
+    }
+    std::pair<size_t, Err> Read(uint8_t *p, size_t n) override {
+        if (r >= b.size()) return {0, Err::EOF_};
+        const size_t k = n < b.size() - r ? n : b.size() - r;
+        std::memcpy(p, b.data() + r, k);
+        r += k;
+        return {k, Err::OK};
+    }
+    void Append(const std::vector<uint8_t> &x) { b.insert(b.end(), x.begin(), x.end()); }
+};
+
+namespace detail {
+inline void panic_if(int st, const char *what) {
+    if (st == EZ_EINVAL) throw Panic(what);
+}
+}  // namespace detail
+
+// ---------------------------------------------------------------- codec
+struct Encoder {  // writer.go:537-621
+    int Ver = 0;
+    void Tag(std::vector<uint8_t> &b, int tag, int64_t l) const { app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_tag(d, c, n, tag, l); }, "Tag"); }
+    void Offset(std::vector<uint8_t> &b, int64_t off, int64_t l) const { app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_offset(d, c, n, off, l); }, "Offset"); }
+    void MetaTag(std::vector<uint8_t> &b, int64_t meta, int64_t l) const { app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_meta(d, c, n, meta, l); }, "Meta"); }
+
+  private:
+    template <class F>
+    static void app(std::vector<uint8_t> &b, F f, const char *what) {
+        const size_t at = b.size();
+        b.resize(at + 16);
+        size_t n = at;
+        const int st = f(b.data(), b.size(), &n);
+        detail::panic_if(st, what);
+        b.resize(n);
+    }
+};
+
+struct Decoder {  // reader.go:346-514; every result carries the next index i (st on error)
+    int Ver = 0;
+    Err Tag(const std::vector<uint8_t> &b, size_t st, int *tag, int64_t *l, size_t *i) const {
+        return (Err)ez_decode_tag(b.data(), b.size(), st, tag, l, i);
+    }
+    Err Offset(const std::vector<uint8_t> &b, size_t st, int64_t l, int64_t *off, size_t *i) const {
+        return (Err)ez_decode_offset(b.data(), b.size(), st, l, off, i);
+    }
+    Err MetaTag(const std::vector<uint8_t> &b, size_t st, int64_t *meta, int64_t *l, size_t *i) const {
+        return (Err)ez_decode_meta(b.data(), b.size(), st, meta, l, i);
+    }
+};
+
+// ---------------------------------------------------------------- Writer
+class Writer {
+  public:
+    IoWriter *W = nullptr;   // Writer.Writer (writer.go:18)
+    bool AppendMagic = true;  // writer.go:23-25
+    int FlushThreshold = 0;   // writer.go:27-34: 0 = each Write, -1 = manual, N = buffered bytes
+    int Ver = 0;              // w.e.Ver
+
+    Writer(IoWriter *w, int64_t block, int64_t htable, int device = 0) : W(w) {
+        const int st = ez_writer_new(block, htable, device, &h_);
+        detail::panic_if(st, "eazy: NewWriter: bad block or htable size");
+        if (st != EZ_OK) throw std::runtime_error(std::string("eazy: NewWriter: ") + ez_strerror(st));
+    }
+    ~Writer() { ez_writer_free(h_); }
+    Writer(const Writer &) = delete;
+    Writer &operator=(const Writer &) = delete;
+
+    // Writer.Write writer.go:206-337: {len(p), OK} or {0, err}.
+    std::pair<size_t, Err> Write(const uint8_t *p, size_t n) {
+        sync();
+        size_t got = 0;
+        const size_t at = b_.size();
+        b_.resize(at + ez_compress_bound(n));
+        const int st = ez_writer_write(h_, p, n, b_.data() + at, b_.size() - at, &got);
+        detail::panic_if(st, "eazy: Write");
+        b_.resize(at + (st == EZ_OK ? got : 0));
+        if (st != EZ_OK) return {0, (Err)st};
+        const Err e = write();
+        if (e != Err::OK) return {0, e};
+        return {n, Err::OK};
+    }
+    std::pair<size_t, Err> Write(const std::vector<uint8_t> &p) { return Write(p.data(), p.size()); }
+    std::pair<size_t, Err> Write(const std::string &p) { return Write((const uint8_t *)p.data(), p.size()); }
+
+    Err WriteHeader() {  // writer.go:342-350
+        if (!isreset()) return Err::OK;
+        return append_call(ez_writer_header);
+    }
+    Err WriteBreak() { return append_call(ez_writer_break); }  // writer.go:358-366
+    Err Flush() { return b_.empty() ? Err::OK : flush(); }      // writer.go:371-377
+    void Reset(IoWriter *w) {                                    // writer.go:149-152
+        W = w;
+        reset();
+    }
+    void ResetSize(IoWriter *w, int64_t block, int64_t htable) {  // writer.go:155-159
+        W = w;
+        detail::panic_if(ez_writer_reset_size(h_, block, htable), "eazy: ResetSize: bad block or htable size");
+        b_.clear();
+        written_ = 0;
+    }
+
+  private:
+    ez_writer *h_ = nullptr;
+    std::vector<uint8_t> b_;  // w.b
+    int64_t written_ = 0;     // w.written
+
+    void sync() {
+        ez_writer_set_append_magic(h_, AppendMagic ? 1 : 0);
+        ez_writer_set_version(h_, Ver);
+    }
+    bool isreset() const { return written_ + (int64_t)b_.size() == 0 && ez_writer_is_reset(h_); }  // writer.go:403-405
+    Err append_call(int (*f)(ez_writer *, uint8_t *, size_t, size_t *)) {
+        sync();
+        const size_t at = b_.size();
+        b_.resize(at + 32);
+        size_t got = 0;
+        const int st = f(h_, b_.data() + at, 32, &got);
+        b_.resize(at + (st == EZ_OK ? got : 0));
+        if (st != EZ_OK) return (Err)st;
+        return write();
+    }
+    void reset() {  // writer.go:187-200
+        ez_writer_reset(h_);
+        b_.clear();
+        written_ = 0;
+    }
+    Err write() {  // writer.go:379-385
+        if (FlushThreshold < 0 || (int64_t)b_.size() < FlushThreshold) return Err::OK;
+        return flush();
+    }
+    Err flush() {  // writer.go:387-401: a failed or short sink write restarts the stream
+        auto [n, err] = W->Write(b_.data(), b_.size());
+        written_ += (int64_t)n;
+        if (err != Err::OK || n != b_.size()) reset();
+        if (err != Err::OK) return err;
+        b_.clear();
+        return Err::OK;
+    }
+};
+
+inline std::unique_ptr<Writer> NewWriter(IoWriter *w, int64_t block, int64_t htable, int device = 0) {
+    return std::make_unique<Writer>(w, block, htable, device);
+}
+
+// ---------------------------------------------------------------- Reader
+class Reader {
+  public:
+    IoReader *R = nullptr;              // Reader.Reader (reader.go:20)
+    int64_t BlockSizeLimit = 16 * MiB;  // NewReader default (reader.go:79-86); NewReaderBytes: 0
+    int BufferSize = 64 * 1024;
+    bool RequireMagic = false;
+    bool SkipUnsupportedMeta = false;
+    int64_t Detail = 0;  // meta id / version of the last UnsupportedMeta / UnsupportedVersion
+
+    explicit Reader(int device = 0) {
+        const int st = ez_reader_new(device, &h_);
+        if (st != EZ_OK) throw std::runtime_error(std::string("eazy: NewReader: ") + ez_strerror(st));
+    }
+    ~Reader() { ez_reader_free(h_); }
+    Reader(const Reader &) = delete;
+    Reader &operator=(const Reader &) = delete;
+
+    void Reset(IoReader *r) {  // reader.go:96-99
+        ResetBytes(nullptr, 0);
+        R = r;
+    }
+    void ResetBytes(const uint8_t *b, size_t n) {  // reader.go:102-113
+        R = nullptr;
+        b_.assign(b, b + n);
+        i_ = 0;
+        boff_ = 0;
+        ez_reader_reset(h_);
+    }
+    void ResetBytes(const std::vector<uint8_t> &b) { ResetBytes(b.data(), b.size()); }
+
+    // Reader.Read reader.go:116-141: data and error together, like Go.
+    std::pair<size_t, Err> Read(uint8_t *p, size_t n) {
+        ez_reader_configure(h_, BlockSizeLimit, RequireMagic ? 1 : 0, SkipUnsupportedMeta ? 1 : 0);
+        size_t got = 0;
+        Err err = Err::OK;
+        while (got < n && err == Err::OK) {
+            size_t m = 0, i = 0;
+            int64_t det = 0;
+            err = (Err)ez_reader_read(h_, b_.data(), b_.size(), i_, boff_, p + got, n - got, &m, &i, &det);
+            if (err == Err::Device) return {got, err};
+            got += m;
+            i_ = i;
+            Detail = det;
+            if (got == n) break;
+            if (err != Err::ShortBuffer) continue;
+            err = more();
+            if (err == Err::EOF_ && (ez_reader_pending(h_) || i_ < b_.size())) err = Err::UnexpectedEOF;
+        }
+        return {got, err};
+    }
+    std::pair<std::vector<uint8_t>, Err> Read(size_t n) {
+        std::vector<uint8_t> p(n);
+        auto [k, e] = Read(p.data(), n);
+        p.resize(k);
+        return {p, e};
+    }
+
+  private:
+    ez_reader *h_ = nullptr;
+    std::vector<uint8_t> b_;  // r.b
+    size_t i_ = 0;            // r.i
+    int64_t boff_ = 0;        // r.boff
+
+    Err more() {  // reader.go:516-543
+        if (!R) return Err::EOF_;
+        b_.erase(b_.begin(), b_.begin() + (ptrdiff_t)i_);
+        boff_ += (int64_t)i_;
+        i_ = 0;
+        const size_t end = b_.size();
+        b_.resize(end + (end == 0 ? (size_t)BufferSize : 1024));
+        auto [k, err] = R->Read(b_.data() + end, b_.size() - end);
+        b_.resize(end + k);
+        if (k != 0 && err == Err::EOF_) err = Err::OK;
+        return err;
+    }
+};
+
+inline std::unique_ptr<Reader> NewReader(IoReader *r, int device = 0) {  // reader.go:79-86
+    auto x = std::make_unique<Reader>(device);
+    x->R = r;
+    return x;
+}
+
+inline std::unique_ptr<Reader> NewReaderBytes(const std::vector<uint8_t> &b, int device = 0) {  // reader.go:89-94
+    auto x = std::make_unique<Reader>(device);
+    x->ResetBytes(b);
+    x->BlockSizeLimit = 0;
+    x->BufferSize = 0;
+    return x;
+}
+
+// ---------------------------------------------------------------- batches (the GPU hot path)
+// One stream per buffer = a fresh NewWriter(block, htable) receiving one
+// Write; device pointers, asynchronous on `hip_stream`.  See include/eazy.h.
+inline Err CompressBatch(int64_t block, int64_t htable, bool append_magic, const ez_batch &b, void *hip_stream) {
+    const int st = ez_compress_batch(block, htable, append_magic ? 0 : EZ_F_NO_MAGIC, &b, hip_stream);
+    detail::panic_if(st, "eazy: CompressBatch: bad block or htable size");
+    return (Err)st;
+}
+inline Err DecompressBatch(int64_t block_size_limit, const ez_batch &b, void *workspace, void *hip_stream) {
+    return (Err)ez_decompress_batch(block_size_limit, &b, workspace, hip_stream);
+}
+
+}  // namespace eazy

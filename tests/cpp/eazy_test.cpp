@@ -1,0 +1,440 @@
+// eazy_test.cpp — the reference's tests (eazy_test.go) restated in C++ over
+// the C++ host side (eazy_amd/cpp/eazy.hpp) and the C-ABI.  Exact-byte
+// expectations are the Go tests' known answers.
+//
+//   ./eazy_test          all tests (needs an MI355X for the Writer/Reader ones)
+//   ./eazy_test --cpu    host-only tests: the token codec, compress bound, ABI
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "../../eazy_amd/cpp/eazy.hpp"
+
+using namespace eazy;
+using Bytes = std::vector<uint8_t>;
+
+static int g_fail = 0, g_run = 0;
+#define CHECK(c)                                                             \
+    do {                                                                     \
+        if (!(c)) {                                                          \
+            std::printf("    %s:%d: CHECK failed: %s\n", __FILE__, __LINE__, #c); \
+            throw 1;                                                         \
+        }                                                                    \
+    } while (0)
+
+static Bytes B(const std::string &s) { return Bytes(s.begin(), s.end()); }
+static Bytes H(const std::string &hex) {
+    Bytes b;
+    for (size_t i = 0; i + 1 < hex.size(); i += 2) b.push_back((uint8_t)std::stoi(hex.substr(i, 2), nullptr, 16));
+    return b;
+}
+static Bytes cat(Bytes a, const Bytes &b) {
+    a.insert(a.end(), b.begin(), b.end());
+    return a;
+}
+static Bytes sub(const Bytes &a, size_t from, size_t to = (size_t)-1) {
+    if (to > a.size()) to = a.size();
+    return Bytes(a.begin() + (ptrdiff_t)from, a.begin() + (ptrdiff_t)to);
+}
+
+static void run(const char *name, const std::function<void()> &f) {
+    g_run++;
+    try {
+        f();
+        std::printf("PASS %s\n", name);
+    } catch (...) {
+        g_fail++;
+        std::printf("FAIL %s\n", name);
+    }
+}
+
+static void write_ok(Writer &w, const Bytes &p) {
+    auto [n, e] = w.Write(p);
+    CHECK(e == Err::OK);
+    CHECK(n == p.size());
+}
+
+static std::pair<Bytes, Err> rd(Reader &r, size_t n) { return r.Read(n); }
+
+// ---------------------------------------------------------------- host-only
+static void TestPrintLengthEncoding() {  // eazy_test.go:1406-1450
+    const std::pair<int64_t, const char *> kat[] = {{1, "01"}, {123, "7b"}, {124, "7c00"}, {379, "7cff"},
+                                                    {380, "7d0000"}, {65915, "7dffff"}, {65916, "7e00000000"}};
+    Encoder e;
+    Decoder d;
+    for (auto &[l, h] : kat) {
+        Bytes b;
+        e.Tag(b, Literal, l);
+        CHECK(b == H(h));
+        int tag = -1;
+        int64_t got = -1;
+        size_t i = 0;
+        CHECK(d.Tag(b, 0, &tag, &got, &i) == Err::OK);
+        CHECK(tag == Literal && got == l && i == b.size());
+    }
+}
+
+static void TestPrintOffsetEncoding() {  // eazy_test.go:1452-1497
+    const std::pair<int64_t, const char *> kat[] = {{1, "01"}, {251, "fb"}, {252, "fc00"}, {507, "fcff"},
+                                                    {508, "fd0000"}, {66043, "fdffff"}, {66044, "fe00000000"}};
+    Encoder e;
+    for (auto &[o, h] : kat) {
+        Bytes b;
+        e.Offset(b, o, 0);
+        CHECK(b == H(h));
+    }
+    Bytes b;
+    e.Offset(b, 5, 10);
+    CHECK(b == H("ff05"));
+    b.clear();
+    e.Offset(b, 20, 10);
+    CHECK(b == H("0a"));
+    int64_t off = 0;
+    size_t i = 0;
+    CHECK(Decoder().Offset(H("fd0365"), 0, 0, &off, &i) == Err::OK);
+    CHECK(off == 26367 && i == 3);  // TestBug1's offset
+}
+
+static void TestReaderShortBuffer() {  // eazy_test.go:858-978
+    Encoder e;
+    Decoder d;
+    for (int64_t tlen : {(int64_t)20, (int64_t)0x100, (int64_t)0x200, (int64_t)0x50000000}) {
+        Bytes b;
+        e.Tag(b, Copy, tlen);
+        for (size_t k = 0; k < b.size(); k++) {
+            int tag = 0;
+            int64_t l = 0;
+            size_t i = 99;
+            CHECK(d.Tag(sub(b, 0, k), 0, &tag, &l, &i) == Err::ShortBuffer);
+            CHECK(i == 0);
+        }
+    }
+    for (int64_t toff : {(int64_t)20, (int64_t)0x100, (int64_t)0x200, (int64_t)0x500, (int64_t)0x50000000}) {
+        for (int64_t l : {(int64_t)10, toff + 10}) {
+            Bytes b;
+            e.Offset(b, toff, l);
+            for (size_t k = 0; k < b.size(); k++) {
+                int64_t off = 0;
+                size_t i = 99;
+                CHECK(d.Offset(sub(b, 0, k), 0, l, &off, &i) == Err::ShortBuffer && i == 0);
+            }
+            int64_t off = 0;
+            size_t i = 0;
+            CHECK(d.Offset(b, 0, l, &off, &i) == Err::OK && off == toff && i == b.size());
+        }
+    }
+    for (int64_t tlen : {(int64_t)0, (int64_t)4, (int64_t)0x80, (int64_t)0x100, (int64_t)0x500, (int64_t)0x50000000}) {
+        Bytes b;
+        e.MetaTag(b, 10 << 3, tlen);
+        for (size_t k = 1; k < b.size(); k++) {
+            int64_t m = 0, l = 0;
+            size_t i = 99;
+            CHECK(d.MetaTag(sub(b, 0, k), 1, &m, &l, &i) == Err::ShortBuffer && i == 1);
+        }
+        int64_t m = 0, l = 0;
+        size_t i = 0;
+        CHECK(d.MetaTag(b, 1, &m, &l, &i) == Err::OK && m == (10 << 3) && l == tlen && i == b.size());
+    }
+}
+
+static void TestEncoderPanics() {  // eazy_test.go:895, 946, TestMeta :814
+    Encoder e;
+    Bytes b;
+    bool p1 = false, p2 = false, p3 = false;
+    try { e.Tag(b, Literal, 0x110000000LL); } catch (const Panic &) { p1 = true; }
+    try { e.Offset(b, 0x110000000LL, 10); } catch (const Panic &) { p2 = true; }
+    try { e.MetaTag(b, 1024, 4); } catch (const Panic &) { p3 = true; }
+    CHECK(p1 && p2 && p3);
+}
+
+static void TestCompressBound() {  // include/eazy.h, tests/test_bound.py
+    for (size_t n : {0UL, 1UL, 4096UL, 1UL << 20})
+        CHECK(ez_compress_bound(n) == n + n / 4 + 32);
+    CHECK(ez_abi_version() == EZ_ABI_VERSION);
+}
+
+// ---------------------------------------------------------------- device
+static void TestMagic() {  // eazy_test.go:39-64
+    Buffer buf;
+    auto w = NewWriter(&buf, MiB, 512);
+    CHECK(w->WriteHeader() == Err::OK);
+    CHECK(buf.b == H("800265617a79801014"));
+    CHECK(w->WriteHeader() == Err::OK);
+    CHECK(buf.b.size() == 9);
+    write_ok(*w, Bytes{0});
+    CHECK(buf.b == H("800265617a7980101401" "00"));
+}
+
+static void TestLiteral() {  // eazy_test.go:66-104
+    Buffer buf;
+    auto w = NewWriter(&buf, 32, 16);
+    w->AppendMagic = false;
+    write_ok(*w, B("very_first_message"));
+    auto r = NewReaderBytes(buf.b);
+    CHECK(rd(*r, 10) == std::make_pair(B("very_first"), Err::OK));
+    CHECK(rd(*r, 10) == std::make_pair(B("_message"), Err::EOF_));
+}
+
+static void TestCopy() {  // eazy_test.go:106-183
+    Buffer buf;
+    auto w = NewWriter(&buf, 32, 16);
+    w->AppendMagic = false;
+    write_ok(*w, B("prefix_1234_suffix"));
+    const size_t st = buf.b.size();
+    write_ok(*w, B("prefix_567_suffix"));
+    CHECK(sub(buf.b, st) == cat(cat(Bytes{Copy | 7, 0x12 - 7, Literal | 3}, B("567")), Bytes{Copy | 7, 0x11 - 7}));
+    CHECK(sub(buf.b, 0, st) == cat(Bytes{Meta, MetaReset, 5, 0x12}, B("prefix_1234_suffix")));
+    auto r = NewReaderBytes(buf.b);
+    CHECK(rd(*r, 10) == std::make_pair(B("prefix_123"), Err::OK));
+    CHECK(rd(*r, 10) == std::make_pair(B("4_suffixpr"), Err::OK));
+    CHECK(rd(*r, 30) == std::make_pair(B("efix_567_suffix"), Err::EOF_));
+}
+
+struct BufNoEOF : IoReader {  // bytes.Buffer: never returns data together with EOF
+    Bytes b;
+    size_t r = 0;
+    std::pair<size_t, Err> Read(uint8_t *p, size_t n) override {
+        if (r >= b.size()) return {0, Err::EOF_};
+        const size_t k = std::min(n, b.size() - r);
+        std::memcpy(p, b.data() + r, k);
+        r += k;
+        return {k, Err::OK};
+    }
+};
+
+static void TestBug1() {  // eazy_test.go:185-207
+    BufNoEOF src;
+    src.b = {Meta, MetaReset, 14, Literal | 3, 0x94, 0xa8, 0xfb, Copy | 9};
+    auto r = NewReader(&src);
+    auto [got, err] = rd(*r, 1000);
+    CHECK(err == Err::UnexpectedEOF);
+    CHECK(got == (Bytes{0x94, 0xa8, 0xfb}));
+    src.b.insert(src.b.end(), {0xfd, 0x03, 0x65});
+    auto [got2, err2] = rd(*r, 1000);
+    CHECK(err2 == Err::Overflow);
+    CHECK(got2.empty());
+}
+
+static void TestPadding() {  // eazy_test.go:209-268
+    Buffer buf;
+    auto w = NewWriter(&buf, 32, 16);
+    write_ok(*w, B("prefix_1234_suffix"));
+    const Bytes head = buf.b;
+    const Bytes pad(32 - head.size() % 32, 0);
+    write_ok(*w, B("prefix_567_suffix"));
+    const Bytes all = cat(cat(head, pad), sub(buf.b, head.size()));
+    auto r = NewReaderBytes(all);
+    CHECK(rd(*r, 10) == std::make_pair(B("prefix_123"), Err::OK));
+    CHECK(rd(*r, 10) == std::make_pair(B("4_suffixpr"), Err::OK));
+    CHECK(rd(*r, 30) == std::make_pair(B("efix_567_suffix"), Err::EOF_));
+}
+
+static void TestZeroRegion() {  // eazy_test.go:270-280
+    auto r = NewReaderBytes(Bytes{Meta, MetaReset, 2, Meta, MetaVer, 0, Copy | 10, OffLong, 0});
+    CHECK(rd(*r, 16) == std::make_pair(Bytes(10, 0), Err::EOF_));
+}
+
+static void TestBreak() {  // eazy_test.go:342-415
+    Buffer buf;
+    auto w = NewWriter(&buf, 32, 16);
+    w->AppendMagic = false;
+    write_ok(*w, B("message1"));
+    CHECK(w->WriteBreak() == Err::OK);
+    write_ok(*w, B("qwessage2"));
+    auto r = NewReaderBytes(buf.b);
+    CHECK(rd(*r, 20) == std::make_pair(B("message1"), Err::Break));
+    CHECK(rd(*r, 20) == std::make_pair(B("qwessage2"), Err::EOF_));
+}
+
+static void TestReaderRequireMagic() {  // eazy_test.go:417-431
+    Buffer buf;
+    auto w = NewWriter(&buf, 1024, 32);
+    w->AppendMagic = false;
+    write_ok(*w, Bytes{0});
+    Buffer src;
+    src.b = buf.b;
+    auto r = NewReader(&src);
+    r->RequireMagic = true;
+    CHECK(rd(*r, 1).second == Err::NoMagic);
+}
+
+static void TestFlush() {  // eazy_test.go:433-491
+    Buffer buf;
+    auto w = NewWriter(&buf, 1024, 32);
+    w->AppendMagic = false;
+    w->FlushThreshold = -1;
+    CHECK(w->WriteHeader() == Err::OK);
+    write_ok(*w, B("aaabbb"));
+    CHECK(w->WriteBreak() == Err::OK);
+    write_ok(*w, B("ccc"));
+    CHECK(buf.b.empty());
+    CHECK(w->Flush() == Err::OK);
+    CHECK(buf.b.size() == 16);
+    CHECK(w->WriteBreak() == Err::OK);
+    CHECK(buf.b.size() == 16);
+    CHECK(w->Flush() == Err::OK);
+    CHECK(buf.b == H("80100a06616161626262801f03636363801f"));
+    Buffer src;
+    src.b = buf.b;
+    auto r = NewReader(&src);
+    CHECK(rd(*r, 10) == std::make_pair(B("aaabbb"), Err::Break));
+    CHECK(rd(*r, 10) == std::make_pair(B("ccc"), Err::Break));
+    CHECK(rd(*r, 10) == std::make_pair(Bytes{}, Err::EOF_));
+}
+
+static void TestFlushReset() {  // eazy_test.go:493-512
+    Buffer buf;
+    auto w = NewWriter(&buf, 1024, 32);
+    w->AppendMagic = false;
+    w->FlushThreshold = -1;
+    write_ok(*w, B("123"));
+    CHECK(buf.b.empty());
+    w->Reset(&buf);
+    w->FlushThreshold = 0;
+    write_ok(*w, B("456"));
+    CHECK(buf.b == H("80100a03343536"));
+}
+
+static void TestRunlenDecoder() {  // eazy_test.go:581-597
+    Buffer src;
+    src.b = H("8010048008000161" "85ff01" "026263" "85ff02" "027878");
+    auto r = NewReader(&src);
+    CHECK(rd(*r, 1000) == std::make_pair(B("aaaaaabcbcbcbxx"), Err::EOF_));
+}
+
+static void TestRunlenEncoder() {  // eazy_test.go:599-670
+    Buffer buf;
+    auto w = NewWriter(&buf, 128, 16);
+    write_ok(*w, Bytes{0});
+    size_t off = buf.b.size();
+    write_ok(*w, B("aaaaaaabcbcbcbcbxx"));
+    CHECK(sub(buf.b, off) == H("016186ff0102626387ff02027878"));
+    Bytes data(0x1005, '0');
+    off = buf.b.size();
+    write_ok(*w, data);
+    CHECK(sub(buf.b, off) == H("0130fd880eff01"));
+    for (size_t k = 3; k < data.size(); k++) data[k] = 0;
+    off = buf.b.size();
+    write_ok(*w, data);
+    CHECK(sub(buf.b, off) == H("03303030fd860eff00"));
+}
+
+static void TestUnsupportedVersion() {  // eazy_test.go:749-762
+    Buffer buf;
+    auto w = NewWriter(&buf, 1024, 32);
+    w->Ver = 1;
+    w->Write(Bytes{1, 2});
+    auto r = NewReaderBytes(buf.b);
+    auto [got, err] = rd(*r, 1);
+    CHECK(err == Err::UnsupportedVersion && got.empty());
+}
+
+struct FailingSink : IoWriter {  // accepts `accept` bytes once, then fails
+    Buffer *dst;
+    long accept = -1;
+    std::pair<size_t, Err> Write(const uint8_t *p, size_t n) override {
+        if (accept < 0) return dst->Write(p, n);
+        const size_t k = std::min(n, (size_t)accept);
+        dst->Write(p, k);
+        accept = -1;
+        return {k, Err::Sink};
+    }
+};
+
+static void TestSinkFailureResets() {  // writer.go:387-401
+    Buffer buf;
+    FailingSink s;
+    s.dst = &buf;
+    auto w = NewWriter(&s, 1024, 32);
+    write_ok(*w, B("first message, first message"));
+    const size_t good = buf.b.size();
+    s.accept = 3;
+    auto [n, e] = w->Write(B("second message"));
+    CHECK(e == Err::Sink && n == 0);
+    CHECK(buf.b.size() == good + 3);
+    const size_t st = buf.b.size();
+    write_ok(*w, B("third message"));
+    CHECK(sub(buf.b, st, st + 6) == H("800265617a79"));  // a fresh stream with its header
+}
+
+static void TestBatchMatchesWriter() {  // the GPU batch path == one NewWriter(MiB,1024).Write per stream
+    std::vector<Bytes> streams;
+    for (int s = 0; s < 40; s++) {
+        Bytes p;
+        for (int k = 0; k < 300 + 97 * s; k++) p.push_back((uint8_t)("level=info path=/api/v1/items "[(k * 7 + s) % 31] ^ (k % 53 == 0 ? s : 0)));
+        streams.push_back(p);
+    }
+    std::vector<uint64_t> in_off{0}, out_off{0};
+    Bytes in;
+    for (auto &p : streams) {
+        in.insert(in.end(), p.begin(), p.end());
+        in_off.push_back(in.size());
+        out_off.push_back(out_off.back() + ez_compress_bound(p.size()));
+    }
+    const size_t count = streams.size();
+    uint8_t *d_in, *d_out;
+    uint64_t *d_in_off, *d_out_off, *d_size;
+    int32_t *d_status;
+    CHECK(hipMalloc(&d_in, in.size() + 16) == hipSuccess);
+    CHECK(hipMalloc(&d_out, out_off.back() + 16) == hipSuccess);
+    CHECK(hipMalloc(&d_in_off, 8 * (count + 1)) == hipSuccess);
+    CHECK(hipMalloc(&d_out_off, 8 * (count + 1)) == hipSuccess);
+    CHECK(hipMalloc(&d_size, 8 * count) == hipSuccess);
+    CHECK(hipMalloc(&d_status, 4 * count) == hipSuccess);
+    (void)hipMemcpy(d_in, in.data(), in.size(), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_in_off, in_off.data(), 8 * (count + 1), hipMemcpyHostToDevice);
+    (void)hipMemcpy(d_out_off, out_off.data(), 8 * (count + 1), hipMemcpyHostToDevice);
+    ez_batch b{d_in, d_in_off, d_out, d_out_off, d_size, d_status, count, 0};
+    CHECK(CompressBatch(MiB, 1024, true, b, nullptr) == Err::OK);
+    CHECK(hipDeviceSynchronize() == hipSuccess);
+    Bytes out(out_off.back());
+    std::vector<uint64_t> size(count);
+    std::vector<int32_t> status(count);
+    (void)hipMemcpy(out.data(), d_out, out.size(), hipMemcpyDeviceToHost);
+    (void)hipMemcpy(size.data(), d_size, 8 * count, hipMemcpyDeviceToHost);
+    (void)hipMemcpy(status.data(), d_status, 4 * count, hipMemcpyDeviceToHost);
+    for (size_t s = 0; s < count; s++) {
+        Buffer buf;
+        auto w = NewWriter(&buf, MiB, 1024);
+        write_ok(*w, streams[s]);
+        CHECK(status[s] == 0);
+        CHECK(sub(out, out_off[s], out_off[s] + size[s]) == buf.b);
+    }
+    for (void *p : {(void *)d_in, (void *)d_out, (void *)d_in_off, (void *)d_out_off, (void *)d_size, (void *)d_status}) (void)hipFree(p);
+}
+
+int main(int argc, char **argv) {
+    const bool cpu = argc > 1 && std::string(argv[1]) == "--cpu";
+    run("TestPrintLengthEncoding", TestPrintLengthEncoding);
+    run("TestPrintOffsetEncoding", TestPrintOffsetEncoding);
+    run("TestReaderShortBuffer", TestReaderShortBuffer);
+    run("TestEncoderPanics", TestEncoderPanics);
+    run("TestCompressBound", TestCompressBound);
+    if (!cpu) {
+        if (ez_device_count() <= 0) {
+            std::printf("FAIL no MI355X visible\n");
+            return 2;
+        }
+        run("TestMagic", TestMagic);
+        run("TestLiteral", TestLiteral);
+        run("TestCopy", TestCopy);
+        run("TestBug1", TestBug1);
+        run("TestPadding", TestPadding);
+        run("TestZeroRegion", TestZeroRegion);
+        run("TestBreak", TestBreak);
+        run("TestReaderRequireMagic", TestReaderRequireMagic);
+        run("TestFlush", TestFlush);
+        run("TestFlushReset", TestFlushReset);
+        run("TestRunlenDecoder", TestRunlenDecoder);
+        run("TestRunlenEncoder", TestRunlenEncoder);
+        run("TestUnsupportedVersion", TestUnsupportedVersion);
+        run("TestSinkFailureResets", TestSinkFailureResets);
+        run("TestBatchMatchesWriter", TestBatchMatchesWriter);
+    }
+    std::printf("%d/%d passed\n", g_run - g_fail, g_run);
+    return g_fail ? 1 : 0;
+}
