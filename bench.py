@@ -41,8 +41,10 @@ def parse():
     ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
     ap.add_argument("--stream-bytes", type=int, default=0, help="override the workload's stream size (experiments)")
     ap.add_argument("--no-check", action="store_true", help="skip the round-trip checks (timing experiments only)")
+    ap.add_argument("--same", action="store_true", help="every stream a copy of stream 0 (divergence experiments)")
     ap.add_argument("--streams", type=int, default=0, help="override the workload's stream count (experiments)")
     ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (rocprofv3 pass)")
     return ap.parse_args()
@@ -95,6 +97,45 @@ def cpu_baseline(host, offs, block, htable, seconds):
     }, first
 
 
+def e2e(ez, data, off, cb, packed, poff, ws, dws, out, osz, ost, block, htable, size, total, comp_bytes, reps=5):
+    """The path as the io.Writer / io.Reader caller sees it: the batch starts
+    and ends in pinned host memory.  compress = H2D(input) + K1 + K3 +
+    D2H(packed); decompress = H2D(packed) + K2 + D2H(output).  Not `value`."""
+    import torch
+
+    h_in = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    h_in.copy_(data[:total].cpu())
+    h_packed = torch.empty(comp_bytes, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    d_in = torch.empty_like(data)
+    d_packed = torch.empty_like(packed)
+
+    def comp():
+        d_in[:total].copy_(h_in, non_blocking=True)
+        ez.compress_batch(d_in, off, block, htable, max_len=size, out=cb)
+        ez.pack(cb, packed, poff, ws)
+        h_packed.copy_(packed[:comp_bytes], non_blocking=True)
+
+    def decomp():
+        d_packed[:comp_bytes].copy_(h_packed, non_blocking=True)
+        ez.decompress_batch(d_packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws)
+        h_out.copy_(out[:total], non_blocking=True)
+
+    t = {}
+    for name, f in (("compress", comp), ("decompress", decomp)):
+        f()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f()
+        torch.cuda.synchronize()
+        t[name] = (time.perf_counter() - t0) / reps
+    assert bool(torch.equal(h_out, h_in)), "host round trip differs"
+    gib = total / 2**30
+    return {"compress_GiBps": gib / t["compress"], "decompress_GiBps": gib / t["decompress"],
+            "note": "pinned host -> HBM -> kernels -> pinned host, hipMemcpyAsync on the compute stream, one rank"}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -123,6 +164,8 @@ def main():
     total = count * size
     host = synth.logs(ezd.seed(1000, R), total)  # this rank's shard of independent streams
     offs = synth.batch_offsets(count, size)
+    if args.same:
+        host = np.tile(host[:size], count)
     data = torch.from_numpy(host).to(dev)
     off = torch.from_numpy(offs).to(dev)
     slot_off = ez.slot_offsets(off)
@@ -189,7 +232,11 @@ def main():
     achieved = alg / (kern[dom] / 1e3) / 1e9
     traffic = None
     if args.traffic_json and os.path.exists(args.traffic_json):
-        traffic = json.load(open(args.traffic_json)).get(dom)
+        # PMC pass of the same command (tools/traffic.py): HBM bytes per launch of the dominant kernel
+        t = json.load(open(args.traffic_json))
+        names = {"k1_compress": ("k1_lane", "k1_g16", "k1_fresh", "k1_compress"), "k2_decompress": ("k2_fast",),
+                 "k3_pack": ("k3_gather",)}[dom]
+        traffic = next((t[n]["traffic"] for n in names if n in t and t[n]["traffic"]), None)
 
     res = {
         "metric": "device-resident compress+decompress GiB/s, 1 MiB block",
@@ -228,6 +275,8 @@ def main():
         },
         "cpu_baseline": None,
     }
+    if not args.no_e2e:
+        res["e2e"] = e2e(ez, data, off, cb, packed, poff, ws, dws, out, osz, ost, block, htable, size, total, comp_bytes)
     if rank == 0 and world == 1 and not args.no_cpu:
         cb_res, first = cpu_baseline(host, offs, block, htable, args.cpu_seconds)
         s0, slots, soff, sizes = first

@@ -13,7 +13,7 @@ for f in sorted(glob.glob(f"{root}/p*/run_counter_collection.csv")):
         k = r["Kernel_Name"]
         if pat not in k:
             continue
-        k = k.split("(")[0].split("::")[-1]
+        k = k.replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1]
         agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r["Dispatch_Id"])
     for k, v in agg.items():

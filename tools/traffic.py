@@ -1,0 +1,34 @@
+"""Per-launch HBM traffic of each kernel from rocprofv3 --pmc passes
+(FETCH_SIZE and WRITE_SIZE in separate passes, KB per dispatch).
+
+gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE counts
+128-B read requests at 64 B, so it is doubled; WRITE_SIZE is taken as is.
+Output: {kernel_name: {"fetch": B, "write": B, "traffic": B}} averaged over
+dispatches, for bench.py --traffic-json."""
+
+import collections
+import csv
+import glob
+import json
+import sys
+
+root, out = sys.argv[1], sys.argv[2]
+acc = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
+    per = collections.defaultdict(float)
+    names = {}
+    for r in csv.DictReader(open(f)):
+        if r["Counter_Name"] not in ("FETCH_SIZE", "WRITE_SIZE"):
+            continue
+        k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].split("::")[-1]
+        per[(k, r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        names[k] = 1
+    for (k, d, c), v in per.items():
+        acc[k][c].append(v * 1024.0)
+res = {}
+for k, v in acc.items():
+    fetch = 2.0 * sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"]) if v["FETCH_SIZE"] else None
+    write = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"]) if v["WRITE_SIZE"] else None
+    res[k] = {"fetch": fetch, "write": write, "traffic": (fetch or 0) + (write or 0) if fetch is not None and write is not None else None}
+json.dump(res, open(out, "w"), indent=1)
+print(json.dumps({k: v for k, v in res.items() if k.startswith("k")}, indent=1))
