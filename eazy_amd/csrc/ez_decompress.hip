@@ -183,247 +183,219 @@ __device__ int d_read_loop(Dec &d, int64_t plen, int64_t *i, int64_t *nout, bool
 // It restates the same reader.go semantics for the common case only: header
 // metas (magic / version 0 / reset before any output), padding, breaks
 // (skipped), literal and copy tokens.  Any other condition — an error of any
-// kind, a mid-stream MetaReset, an unsupported or wide meta, a reference
-// before the stream start, a length over BlockSizeLimit, a full output slot,
-// a truncated token — hands the stream to the exact wave-per-stream decoder
-// (k2_decompress over A.slow), which recomputes it from scratch.
+// kind, a mid-stream MetaReset, an unsupported or wide meta, a length over
+// BlockSizeLimit, a full output slot, a truncated token — hands the stream to
+// the exact wave-per-stream decoder (k2_decompress over A.slow), which
+// recomputes it from scratch.
+//
+// Lanes of a wave sit at different points of different streams, so the loop
+// body is written to be uniform: every lane runs the same instruction
+// sequence each iteration (parse by selects, one predicated 16-byte load,
+// one 16-byte store); only rare events (metas, slot tails, errors) branch.
 
 typedef uint4 __attribute__((aligned(1))) uint4_u;
-typedef unsigned __int128 u128;
 
-__device__ __forceinline__ u128 to128(uint4 v) {
-    return ((u128)((uint64_t)v.z | ((uint64_t)v.w << 32)) << 64) | ((uint64_t)v.x | ((uint64_t)v.y << 32));
-}
-__device__ __forceinline__ uint4 from128(u128 x) {
-    const uint64_t lo = (uint64_t)x, hi = (uint64_t)(x >> 64);
-    return make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
-}
-__device__ __forceinline__ uint4 ld16(const uint8_t *p) { return *(const uint4_u *)p; }
-__device__ __forceinline__ void st16(uint8_t *p, uint4 v) { *(uint4_u *)p = v; }
-__device__ __forceinline__ uint32_t bat(u128 h, uint32_t k) { return (uint32_t)(h >> (8 * k)) & 0xff; }
-__device__ __forceinline__ uint32_t le32at(u128 h, uint32_t k) { return (uint32_t)(h >> (8 * k)); }
+struct V16 {
+    uint64_t lo, hi;
+};
 
-// 16 input bytes at q (q < end), never reading at or past `end` (bytes there
-// read as 0): one clamped load shifted into place.  The launcher routes
-// batches under 16 input bytes to the exact decoder.
-__device__ __forceinline__ u128 ld_in(const uint8_t *q, const uint8_t *end) {
-    const int64_t over = (q + 16) - end;
-    if (over <= 0) return to128(ld16(q));
-    const u128 x = to128(ld16(end - 16));
-    return over >= 16 ? (u128)0 : x >> (8 * over);
+__device__ __forceinline__ V16 ld16v(const uint8_t *p) {
+    const uint4 v = *(const uint4_u *)p;
+    return {(uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z | ((uint64_t)v.w << 32)};
 }
-
-// 16 bytes of a stream's output history at y (y < dst): bytes before the
-// slot start read as 0 (the decoder's fresh window, reader.go:176-196).
-// Needs a slot of at least 16 bytes when y < 0.
-__device__ __forceinline__ u128 ld_hist(const uint8_t *out, int64_t y) {
-    if (y >= 0) return to128(ld16(out + y));
-    if (y <= -16) return 0;
-    return to128(ld16(out)) << (8 * -y);
+__device__ __forceinline__ void st16v(uint8_t *p, V16 v) {
+    *(uint4_u *)p = make_uint4((uint32_t)v.lo, (uint32_t)(v.lo >> 32), (uint32_t)v.hi, (uint32_t)(v.hi >> 32));
 }
-
-// k < 16 bytes of x at d: 8/4/2/1-byte stores, no loop
-__device__ __forceinline__ void put_small(uint8_t *d, u128 x, int64_t k) {
+// shifts that saturate to 0 at >= 64 bits (selects, no branches)
+__device__ __forceinline__ uint64_t shr64(uint64_t a, uint32_t n) { return n >= 64 ? 0 : a >> (n & 63); }
+__device__ __forceinline__ uint64_t shl64(uint64_t a, uint32_t n) { return n >= 64 ? 0 : a << (n & 63); }
+// bytes s .. s+7 of the 16 bytes (a, b), 0 <= s <= 7
+__device__ __forceinline__ uint64_t fun8(uint64_t a, uint64_t b, uint32_t s) {
+    return (a >> (8 * s)) | shl64(b, 64 - 8 * s);
+}
+// v shifted towards lower addresses by k bytes (k >= 0), zeros shifted in
+__device__ __forceinline__ V16 shr16(V16 v, uint32_t k) {
+    const uint32_t n = 8 * (k < 16 ? k : 16);
+    const uint64_t lo = n < 64 ? shr64(v.lo, n) | shl64(v.hi, 64 - n) : shr64(v.hi, n - 64);
+    return {lo, n < 64 ? shr64(v.hi, n) : 0};
+}
+// v shifted towards higher addresses by k bytes (k >= 0), zeros shifted in
+__device__ __forceinline__ V16 shl16(V16 v, uint32_t k) {
+    const uint32_t n = 8 * (k < 16 ? k : 16);
+    const uint64_t hi = n < 64 ? shl64(v.hi, n) | shr64(v.lo, 64 - n) : shl64(v.lo, n - 64);
+    return {n < 64 ? shl64(v.lo, n) : 0, hi};
+}
+// 16 bytes at y, clamped into [lo, hi) (hi - lo >= 16): bytes outside read as 0
+__device__ __forceinline__ V16 ld_clamped(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
+    const uint8_t *yc = y < lo ? lo : (y > hi - 16 ? hi - 16 : y);
+    const V16 v = ld16v(yc);
+    const int64_t d = y - yc;
+    const V16 r = shr16(v, (uint32_t)(d > 0 ? d : 0)), l = shl16(v, (uint32_t)(d < 0 ? -d : 0));
+    return d >= 0 ? r : l;
+}
+// the low `per` bytes of v (1 <= per < 16) repeated over 16 bytes
+__device__ __forceinline__ V16 run_pattern(V16 v, uint32_t per) {
+    V16 x = per >= 8 ? V16{v.lo, per == 8 ? 0 : v.hi & ((1ull << (8 * (per - 8))) - 1)} : V16{v.lo & ((1ull << (8 * per)) - 1), 0};
+#pragma unroll
+    for (int t = 0; t < 4; t++) {  // span = per << t; shl16 by >= 16 bytes is a no-op (zero)
+        const V16 y = shl16(x, per << t);
+        x.lo |= y.lo;
+        x.hi |= y.hi;
+    }
+    return x;
+}
+// k < 16 bytes of v at d: 8/4/2/1-byte stores, no loop
+__device__ __forceinline__ void put_small(uint8_t *d, V16 v, uint32_t k) {
     typedef uint64_t __attribute__((aligned(1))) u64_u;
     typedef uint32_t __attribute__((aligned(1))) u32_u;
     typedef uint16_t __attribute__((aligned(1))) u16_u;
-    int64_t o = 0;
-    if (k & 8) { *(u64_u *)(d + o) = (uint64_t)x; x >>= 64; o += 8; }
+    uint32_t o = 0;
+    uint64_t x = v.lo;
+    if (k & 8) { *(u64_u *)(d + o) = x; x = v.hi; o += 8; }
     if (k & 4) { *(u32_u *)(d + o) = (uint32_t)x; x >>= 32; o += 4; }
     if (k & 2) { *(u16_u *)(d + o) = (uint16_t)x; x >>= 16; o += 2; }
     if (k & 1) d[o] = (uint8_t)x;
 }
 
-// One iteration = (parse the next token from registers when the previous one
-// is written) + (one 16-byte move).  All loads of an iteration — the move's
-// source and the prefetch of the next 16 compressed bytes — are issued
-// together, so a lane waits for memory once per iteration.
 #ifndef EZ_EXP
 #define EZ_EXP 0  // timing experiments only (1: no stores, 2: no data loads, 3: neither)
 #endif
-enum : int { M_REG = 0, M_IN = 1, M_OUT = 2, M_PAT = 3, M_PATLD = 4 };
 
-// the low `per` bytes of x (1 <= per < 16) repeated over 16 bytes
-__device__ __forceinline__ u128 run_pattern(u128 x, int32_t per) {
-    x &= ((u128)1 << (8 * per)) - 1;
-    x |= x << (8 * per);
-    if (2 * per < 16) x |= x << (16 * per);
-    if (4 * per < 16) x |= x << (32 * per);
-    if (8 * per < 16) x |= x << (64 * per);
-    return x;
-}
-
-__global__ __launch_bounds__(256) void k2_fast(DecompressArgs A) {
-    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= A.count) return;
+// One iteration = (parse the token whose header was loaded by the previous
+// iteration) + (one 16-byte move).  The move's source load and the next
+// header's load are issued together: a lane waits for memory once per
+// iteration, and the hardware's unaligned loads do all byte alignment.
+// Rare cases (metas, long lengths, runs shorter than 16, references before
+// the slot, the batch's last bytes, slot tails) take branches.
+__device__ __forceinline__ void fast_one(const DecompressArgs &A, const uint64_t s) {
     const uint8_t *b = A.in + A.in_off[s];
-    int64_t nb = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
+    const int64_t nb64 = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
     const uint8_t *in_end = A.in + A.in_off[A.count];  // loads never pass the last stream's end
     uint8_t *out = A.out + A.out_off[s];
-    const int64_t cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    const int64_t cap64 = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
     const int64_t limit = A.block_size_limit;
-    int64_t i = 0, pos = 0, bs = 0;
-    bool slow = in_end - A.in < 16;  // ld_in's clamped loads need 16 input bytes
-    // register window over the compressed stream: bytes [wb, wb + 32); i - wb < 16 at a parse
-    int64_t wb = 0;
-    u128 c0 = 0, c1 = 0;
-    if (!slow) {
-        c0 = ld_in(b, in_end);
-        c1 = ld_in(b + 16, in_end);
-    } else {
-        nb = 0;  // skip the loop: the exact decoder takes the stream
-    }
-    // the token being written: rem bytes at out + dst, from src (input or output offset)
-    int64_t rem = 0, dst = 0, src = 0, Dd = 16;
-    int32_t per = 0;
-    int mode = M_REG;
+    // 32-bit positions; clamped loads need >= 16 input bytes in the batch and a 16-byte slot
+    bool slow = in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16;
+    const int32_t nb = slow ? 0 : (int32_t)nb64, cap = (int32_t)cap64;
+    int32_t i = 0, pos = 0, bsl = -1;  // bsl: log2 of the window after MetaReset (-1: none yet)
+    V16 h{0, 0};                       // 16 bytes at b + i (the next header)
+    if (!slow) h = b + 16 <= in_end ? ld16v(b) : ld_clamped(b, A.in, in_end);
+    // the token being written: rem bytes at out + dst from src (input or output)
+    int32_t rem = 0, dst = 0, src = 0, step = 16;
+    bool from_in = false, patt = false;
+    V16 pv{0, 0};
 #if EZ_EXP == 1 || EZ_EXP == 3
-    u128 sinkv = 0;
+    uint64_t sinkv = 0;
 #endif
-    u128 v = 0;
     for (;;) {
         if (rem == 0) {
             if (i >= nb) break;
-            const int64_t r = i - wb;
-            const u128 h = r ? (c0 >> (8 * r)) | (c1 << (128 - 8 * r)) : c0;  // bytes i .. i+15
-            const uint32_t t0 = (uint32_t)h & 0xff;
+            const uint64_t lo = h.lo;
+            const uint32_t t0 = (uint32_t)lo & 0xff, l7 = t0 & 0x7f;
+            int32_t adv;
             if (t0 == 0) {  // padding (reader.go:221-224), a run of zero bytes at once
-                const uint64_t lo = (uint64_t)h, hi = (uint64_t)(h >> 64);
-                i += lo ? (__builtin_ctzll(lo) >> 3) : (hi ? 8 + (__builtin_ctzll(hi) >> 3) : 16);
+                adv = lo ? (int32_t)(__builtin_ctzll(lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
+            } else if ((t0 & 0x80) && l7 == 0) {
+                // meta (continueMetaTag reader.go:272-325): header metas and breaks only
+                const uint32_t mb = (uint32_t)(lo >> 8) & 0xff, mt = mb & 0xf8, ml = mb & 7;
+                const int32_t mln = ml == 7 ? 0 : (1 << ml);
+                const uint32_t marg = (uint32_t)(lo >> 16) & 0xff;
+                const bool m_brk = mt == kMetaBreak && mln == 0;
+                const bool m_rst = mt == kMetaReset && mln == 1 && marg <= 32 && pos == 0 && (limit == 0 || (1ll << marg) <= limit);
+                const bool m_ver = mt == kMetaVer && mln == 1 && marg == 0;
+                const bool m_mag = mt == kMetaMagic && mln == 4 && (uint32_t)(lo >> 16) == 0x797a6165u;
+                if (ml == 6 || i + 2 + mln > nb || !(m_brk || m_rst || m_ver || m_mag)) { slow = true; break; }
+                if (m_rst) bsl = (int32_t)marg;
+                adv = 2 + mln;
             } else {
                 // Decoder.Tag reader.go:346-392
-                const uint32_t l7 = t0 & 0x7f;
                 int64_t L;
                 uint32_t j;
                 if (l7 < 124) { L = l7; j = 1; }
-                else if (l7 == 124) { L = 124 + bat(h, 1); j = 2; }
-                else if (l7 == 125) { L = 380 + (le32at(h, 1) & 0xffff); j = 3; }
-                else if (l7 == 126) { L = 65916 + (int64_t)le32at(h, 1); j = 5; }
+                else if (l7 == 124) { L = 124 + (int64_t)((lo >> 8) & 0xff); j = 2; }
+                else if (l7 == 125) { L = 380 + (int64_t)((lo >> 8) & 0xffff); j = 3; }
+                else if (l7 == 126) { L = 65916 + (int64_t)(uint32_t)(lo >> 8); j = 5; }
                 else { slow = true; break; }  // LenAlt -> ErrOverflow
+                const int64_t bs = bsl < 0 ? 0 : (1ll << bsl);
+                if ((limit != 0 && L > limit) || bs == 0 || pos + L > cap) { slow = true; break; }
+                dst = pos;
+                rem = (int32_t)L;
+                pos += (int32_t)L;
+                step = 16;
+                patt = false;
                 if (t0 & 0x80) {
-                    if (L == 0) {
-                        // meta (continueMetaTag reader.go:272-325)
-                        if (i + 2 > nb) { slow = true; break; }
-                        const uint32_t m = bat(h, 1);
-                        const uint32_t meta = m & 0xf8, ml = m & 7;
-                        int64_t ln;
-                        if (ml == 7) ln = 0;
-                        else if (ml < 6) ln = (int64_t)1 << ml;
-                        else { slow = true; break; }  // wide meta length
-                        if (i + 2 + ln > nb) { slow = true; break; }
-                        if (meta == kMetaBreak && ln == 0) {
-                            i += 2;  // ErrBreak: skipped in a batch
-                        } else if (meta == kMetaReset && ln == 1) {
-                            const uint32_t bsl = bat(h, 2);
-                            if (bsl > 32 || (limit != 0 && ((int64_t)1 << bsl) > limit) || pos != 0) { slow = true; break; }
-                            bs = (int64_t)1 << bsl;
-                            i += 3;
-                        } else if (meta == kMetaVer && ln == 1 && bat(h, 2) == 0) {
-                            i += 3;
-                        } else if (meta == kMetaMagic && ln == 4 && le32at(h, 2) == 0x797a6165u) {
-                            i += 6;
+                    // Decoder.Offset reader.go:394-420; the header is <= 11 bytes
+                    const uint64_t x = fun8(lo, h.hi, j);  // bytes from the offset on
+                    const bool lng = (x & 0xff) == 0xff;
+                    const uint64_t y = lng ? fun8(lo, h.hi, j + 1) : x;
+                    const uint32_t o = (uint32_t)y & 0xff;
+                    int64_t D;
+                    uint32_t k;
+                    if (o < 252) { D = o; k = 1; }
+                    else if (o == 252) { D = 252 + (int64_t)((y >> 8) & 0xff); k = 2; }
+                    else if (o == 253) { D = 508 + (int64_t)((y >> 8) & 0xffff); k = 3; }
+                    else if (o == 254) { D = 66044 + (int64_t)(uint32_t)(y >> 8); k = 5; }
+                    else { slow = true; break; }  // OffAlt
+                    if (!lng) D += L;
+                    adv = (int32_t)(j + (lng ? 1 : 0) + k);
+                    if (i + adv > nb || D > bs) { slow = true; break; }
+                    from_in = false;
+                    src = dst - (int32_t)D;
+                    if (D < 16) {
+                        // zero region (D == 0, reader.go:176-179) or a short-period run:
+                        // one 16-byte pattern stored every `step` bytes
+                        patt = true;
+                        if (D == 0) {
+                            pv = V16{0, 0};
                         } else {
-                            slow = true;  // an error or an unsupported meta
-                            break;
-                        }
-                    } else {
-                        // Decoder.Offset reader.go:394-420
-                        if (limit != 0 && L > limit) { slow = true; break; }
-                        uint32_t o = bat(h, j);
-                        const bool lng = o == 0xff;
-                        if (lng) { j++; o = bat(h, j); }
-                        int64_t D;
-                        if (o < 252) { D = o; j += 1; }
-                        else if (o == 252) { D = 252 + bat(h, j + 1); j += 2; }
-                        else if (o == 253) { D = 508 + (le32at(h, j + 1) & 0xffff); j += 3; }
-                        else if (o == 254) { D = 66044 + (int64_t)le32at(h, j + 1); j += 5; }
-                        else { slow = true; break; }  // OffAlt
-                        if (!lng) D += L;
-                        if (i + j > nb || bs == 0 || D > bs || pos + L > cap || (D > pos && cap < 16)) { slow = true; break; }
-                        i += j;
-                        dst = pos;
-                        rem = L;
-                        pos += L;
-                        Dd = 16;
-                        if (D == 0) {  // zero region (reader.go:176-179)
-                            mode = M_REG;
-                            v = 0;
-                        } else if (D < 16) {  // short-period run: a 16-byte pattern every Dd bytes
-                            Dd = D * (16 / D);
-                            per = (int32_t)D;
-                            mode = M_PATLD;
-                            src = dst - 16;
-                        } else {
-                            mode = M_OUT;
-                            src = dst - D;
+                            const uint32_t per = (uint32_t)D;
+                            pv = run_pattern(shr16(ld_clamped(out + dst - 16, out, out + cap), 16 - per), per);
+                            step = (int32_t)(per * (16 / per));
                         }
                     }
                 } else {
                     // literal (reader.go:170-172)
-                    if (limit != 0 && L > limit) { slow = true; break; }
-                    if (bs == 0 || i + j + L > nb || pos + L > cap) { slow = true; break; }
-                    dst = pos;
-                    rem = L;
-                    pos += L;
-                    Dd = 16;
-                    if (j + L <= 16) {  // bytes straight from the header window
-                        mode = M_REG;
-                        v = h >> (8 * j);
-                    } else {
-                        mode = M_IN;
-                        src = i + j;
-                    }
-                    i += j + L;
+                    adv = (int32_t)(j + L);
+                    if ((int64_t)i + j + L > nb) { slow = true; break; }
+                    from_in = true;
+                    src = i + (int32_t)j;
                 }
             }
+            i += adv;
+            // the next header, loaded beside this token's first move
+            if (i < nb) h = b + i + 16 <= in_end ? ld16v(b + i) : ld_clamped(b + i, A.in, in_end);
         }
-        // ---- loads of this iteration, issued together ----
-        u128 raw = 0;
-#if EZ_EXP != 2 && EZ_EXP != 3
-        if (rem > 0 && (mode == M_IN || mode == M_OUT || mode == M_PATLD))
-            raw = mode == M_IN ? ld_in(b + src, in_end) : ld_hist(out, src);
-#else
-        raw = c0 ^ (u128)src;
-#endif
-        const bool rebase = i - wb >= 32;
-        u128 n0 = 0, n1 = 0;
-        if (rebase) {
-            n0 = ld_in(b + i, in_end);
-            n1 = ld_in(b + i + 16, in_end);
-        } else if (i - wb >= 16) {
-            n1 = ld_in(b + wb + 32, in_end);
-        }
-        // ---- the move ----
         if (rem > 0) {
-            if (mode == M_PATLD) {  // raw = the 16 bytes before dst; the period is its top `per` bytes
-                v = run_pattern(raw >> (8 * (16 - per)), per);
-                mode = M_PAT;
-            } else if (mode != M_REG && mode != M_PAT) {
-                v = raw;
+            V16 v;
+            if (patt) {
+                v = pv;
+            } else if (from_in) {
+#if EZ_EXP != 2 && EZ_EXP != 3
+                v = b + src + 16 <= in_end ? ld16v(b + src) : ld_clamped(b + src, A.in, in_end);
+#else
+                v = V16{(uint64_t)src, h.lo};
+#endif
+            } else {
+#if EZ_EXP != 2 && EZ_EXP != 3
+                v = src >= 0 ? ld16v(out + src) : ld_clamped(out + src, out, out + cap);  // before the slot: zeros
+#else
+                v = V16{(uint64_t)src, h.lo};
+#endif
             }
 #if EZ_EXP != 1 && EZ_EXP != 3
-            if (rem >= 16 || dst + 16 <= cap) st16(out + dst, from128(v));
-            else put_small(out + dst, v, rem);
+            if (rem >= 16 || dst + 16 <= cap) st16v(out + dst, v);
+            else put_small(out + dst, v, (uint32_t)rem);
 #else
-            sinkv ^= v;
+            sinkv ^= v.lo;
 #endif
-            const int64_t step = rem < Dd ? rem : Dd;
-            dst += step;
-            src += step;
-            rem -= step;
-        }
-        if (rebase) {
-            wb = i;
-            c0 = n0;
-            c1 = n1;
-        } else if (i - wb >= 16) {
-            wb += 16;
-            c0 = c1;
-            c1 = n1;
+            const int32_t k = rem < step ? rem : step;
+            dst += k;
+            src += k;
+            rem -= k;
         }
     }
 #if EZ_EXP == 1 || EZ_EXP == 3
-    if ((uint64_t)sinkv == 0x123456789ull) pos++;
+    if (sinkv == 0x123456789ull) pos++;
 #endif
     if (slow) {
         const uint32_t at = atomicAdd(&A.slow[0], 1u);
@@ -432,6 +404,12 @@ __global__ __launch_bounds__(256) void k2_fast(DecompressArgs A) {
         A.out_size[s] = (uint64_t)pos;
         if (A.status) A.status[s] = EZ_OK;
     }
+}
+
+// grid-stride over streams (EZ_K2_WAVES caps the streams in flight, experiments)
+__global__ __launch_bounds__(256) void k2_fast(DecompressArgs A) {
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < A.count; s += (uint64_t)gridDim.x * blockDim.x)
+        fast_one(A, s);
 }
 
 __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
@@ -503,7 +481,10 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     static const unsigned blk = getenv("EZ_K2_BLOCK") ? (unsigned)atoi(getenv("EZ_K2_BLOCK")) : 256u;
-    hipLaunchKernelGGL(k2_fast, dim3((unsigned)((a.count + blk - 1) / blk)), dim3(blk), 0, st, a);
+    static const uint64_t maxw = getenv("EZ_K2_WAVES") ? (uint64_t)atoll(getenv("EZ_K2_WAVES")) : 0;
+    uint64_t fgrid = (a.count + blk - 1) / blk;
+    if (maxw && fgrid * blk / 64 > maxw) fgrid = (maxw * 64 + blk - 1) / blk;
+    hipLaunchKernelGGL(k2_fast, dim3((unsigned)fgrid), dim3(blk), 0, st, a);
     // exact decoder over the handed-over streams (count read on the device)
     uint64_t grid = a.count < 4096 ? a.count : 4096;
     hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
