@@ -280,8 +280,9 @@ __device__ __forceinline__ void fast_one(const DecompressArgs &A, const uint64_t
     int32_t i = 0, pos = 0, bsl = -1;  // bsl: log2 of the window after MetaReset (-1: none yet)
     V16 h{0, 0};                       // 16 bytes at b + i (the next header)
     if (!slow) h = b + 16 <= in_end ? ld16v(b) : ld_clamped(b, A.in, in_end);
-    // the token being written: rem bytes at out + dst from src (input or output)
-    int32_t rem = 0, dst = 0, src = 0, step = 16;
+    // the token being written: rem bytes at out + dst from sp (input or output)
+    int32_t rem = 0, dst = 0, step = 16;
+    const uint8_t *sp = b;
     bool from_in = false, patt = false;
     V16 pv{0, 0};
 #if EZ_EXP == 1 || EZ_EXP == 3
@@ -293,72 +294,58 @@ __device__ __forceinline__ void fast_one(const DecompressArgs &A, const uint64_t
             const uint64_t lo = h.lo;
             const uint32_t t0 = (uint32_t)lo & 0xff, l7 = t0 & 0x7f;
             int32_t adv;
-            if (t0 == 0) {  // padding (reader.go:221-224), a run of zero bytes at once
-                adv = lo ? (int32_t)(__builtin_ctzll(lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
-            } else if ((t0 & 0x80) && l7 == 0) {
-                // meta (continueMetaTag reader.go:272-325): header metas and breaks only
-                const uint32_t mb = (uint32_t)(lo >> 8) & 0xff, mt = mb & 0xf8, ml = mb & 7;
-                const int32_t mln = ml == 7 ? 0 : (1 << ml);
-                const uint32_t marg = (uint32_t)(lo >> 16) & 0xff;
-                const bool m_brk = mt == kMetaBreak && mln == 0;
-                const bool m_rst = mt == kMetaReset && mln == 1 && marg <= 32 && pos == 0 && (limit == 0 || (1ll << marg) <= limit);
-                const bool m_ver = mt == kMetaVer && mln == 1 && marg == 0;
-                const bool m_mag = mt == kMetaMagic && mln == 4 && (uint32_t)(lo >> 16) == 0x797a6165u;
-                if (ml == 6 || i + 2 + mln > nb || !(m_brk || m_rst || m_ver || m_mag)) { slow = true; break; }
-                if (m_rst) bsl = (int32_t)marg;
-                adv = 2 + mln;
+            if (t0 == 0 || t0 == 0x80) {
+                if (t0 == 0) {  // padding (reader.go:221-224), a run of zero bytes at once
+                    adv = lo ? (int32_t)(__builtin_ctzll(lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
+                } else {
+                    // meta (continueMetaTag reader.go:272-325): header metas and breaks only
+                    const uint32_t mb = (uint32_t)(lo >> 8) & 0xff, mt = mb & 0xf8, ml = mb & 7;
+                    const int32_t mln = ml == 7 ? 0 : (1 << ml);
+                    const uint32_t marg = (uint32_t)(lo >> 16) & 0xff;
+                    const bool m_brk = mt == kMetaBreak && mln == 0;
+                    const bool m_rst = mt == kMetaReset && mln == 1 && marg <= 32 && pos == 0 && (limit == 0 || (1ll << marg) <= limit);
+                    const bool m_ver = mt == kMetaVer && mln == 1 && marg == 0;
+                    const bool m_mag = mt == kMetaMagic && mln == 4 && (uint32_t)(lo >> 16) == 0x797a6165u;
+                    if (ml == 6 || i + 2 + mln > nb || !(m_brk || m_rst || m_ver || m_mag)) { slow = true; break; }
+                    if (m_rst) bsl = (int32_t)marg;
+                    adv = 2 + mln;
+                }
             } else {
-                // Decoder.Tag reader.go:346-392
-                int64_t L;
-                uint32_t j;
-                if (l7 < 124) { L = l7; j = 1; }
-                else if (l7 == 124) { L = 124 + (int64_t)((lo >> 8) & 0xff); j = 2; }
-                else if (l7 == 125) { L = 380 + (int64_t)((lo >> 8) & 0xffff); j = 3; }
-                else if (l7 == 126) { L = 65916 + (int64_t)(uint32_t)(lo >> 8); j = 5; }
-                else { slow = true; break; }  // LenAlt -> ErrOverflow
+                // Decoder.Tag reader.go:346-392 and Decoder.Offset :394-420, by selects
+                const uint32_t lx = (uint32_t)(lo >> 8);
+                const int64_t L = l7 < 124 ? (int64_t)l7
+                                : (l7 == 124 ? 124 + (int64_t)(lx & 0xff) : (l7 == 125 ? 380 + (int64_t)(lx & 0xffff) : 65916 + (int64_t)lx));
+                const uint32_t j = l7 < 124 ? 1 : (l7 == 124 ? 2 : (l7 == 125 ? 3 : 5));
+                const bool cp = (t0 & 0x80) != 0;
+                const uint64_t x = fun8(lo, h.hi, j);  // bytes from the offset on (header <= 11 bytes)
+                const bool lng = (x & 0xff) == 0xff;
+                const uint64_t y = lng ? fun8(lo, h.hi, j + 1) : x;
+                const uint32_t o = (uint32_t)y & 0xff, ox = (uint32_t)(y >> 8);
+                const int64_t D0 = o < 252 ? (int64_t)o : (o == 252 ? 252 + (int64_t)(ox & 0xff) : (o == 253 ? 508 + (int64_t)(ox & 0xffff) : 66044 + (int64_t)ox));
+                const uint32_t k = o < 252 ? 1 : (o == 252 ? 2 : (o == 253 ? 3 : 5));
+                const int64_t D = lng ? D0 : D0 + L;
+                adv = cp ? (int32_t)(j + (lng ? 1 : 0) + k) : (int32_t)(j + L);
                 const int64_t bs = bsl < 0 ? 0 : (1ll << bsl);
-                if ((limit != 0 && L > limit) || bs == 0 || pos + L > cap) { slow = true; break; }
+                const bool bad = l7 == 127 || (cp && o == 255) || (limit != 0 && L > limit) || bs == 0 ||
+                                 pos + L > cap || (int64_t)i + (cp ? (int64_t)adv : (int64_t)j + L) > nb || (cp && D > bs);
+                if (bad) { slow = true; break; }  // the exact decoder takes the stream
                 dst = pos;
                 rem = (int32_t)L;
                 pos += (int32_t)L;
+                from_in = !cp;
+                sp = cp ? out + (dst - (int32_t)D) : b + (i + (int32_t)j);
+                patt = cp && D < 16;
                 step = 16;
-                patt = false;
-                if (t0 & 0x80) {
-                    // Decoder.Offset reader.go:394-420; the header is <= 11 bytes
-                    const uint64_t x = fun8(lo, h.hi, j);  // bytes from the offset on
-                    const bool lng = (x & 0xff) == 0xff;
-                    const uint64_t y = lng ? fun8(lo, h.hi, j + 1) : x;
-                    const uint32_t o = (uint32_t)y & 0xff;
-                    int64_t D;
-                    uint32_t k;
-                    if (o < 252) { D = o; k = 1; }
-                    else if (o == 252) { D = 252 + (int64_t)((y >> 8) & 0xff); k = 2; }
-                    else if (o == 253) { D = 508 + (int64_t)((y >> 8) & 0xffff); k = 3; }
-                    else if (o == 254) { D = 66044 + (int64_t)(uint32_t)(y >> 8); k = 5; }
-                    else { slow = true; break; }  // OffAlt
-                    if (!lng) D += L;
-                    adv = (int32_t)(j + (lng ? 1 : 0) + k);
-                    if (i + adv > nb || D > bs) { slow = true; break; }
-                    from_in = false;
-                    src = dst - (int32_t)D;
-                    if (D < 16) {
-                        // zero region (D == 0, reader.go:176-179) or a short-period run:
-                        // one 16-byte pattern stored every `step` bytes
-                        patt = true;
-                        if (D == 0) {
-                            pv = V16{0, 0};
-                        } else {
-                            const uint32_t per = (uint32_t)D;
-                            pv = run_pattern(shr16(ld_clamped(out + dst - 16, out, out + cap), 16 - per), per);
-                            step = (int32_t)(per * (16 / per));
-                        }
+                if (patt) {
+                    // zero region (D == 0, reader.go:176-179) or a short-period run:
+                    // one 16-byte pattern stored every `step` bytes
+                    if (D == 0) {
+                        pv = V16{0, 0};
+                    } else {
+                        const uint32_t per = (uint32_t)D;
+                        pv = run_pattern(shr16(ld_clamped(out + dst - 16, out, out + cap), 16 - per), per);
+                        step = (int32_t)(per * (16 / per));
                     }
-                } else {
-                    // literal (reader.go:170-172)
-                    adv = (int32_t)(j + L);
-                    if ((int64_t)i + j + L > nb) { slow = true; break; }
-                    from_in = true;
-                    src = i + (int32_t)j;
                 }
             }
             i += adv;
@@ -367,31 +354,24 @@ __device__ __forceinline__ void fast_one(const DecompressArgs &A, const uint64_t
         }
         if (rem > 0) {
             V16 v;
-            if (patt) {
-                v = pv;
-            } else if (from_in) {
 #if EZ_EXP != 2 && EZ_EXP != 3
-                v = b + src + 16 <= in_end ? ld16v(b + src) : ld_clamped(b + src, A.in, in_end);
+            // inputs near the batch end / references before the slot read zeros there (rare)
+            if (from_in ? sp + 16 > in_end : sp < out) v = from_in ? ld_clamped(sp, A.in, in_end) : ld_clamped(sp, out, out + cap);
+            else v = ld16v(sp);
 #else
-                v = V16{(uint64_t)src, h.lo};
+            v = V16{(uint64_t)sp, h.lo};
 #endif
-            } else {
-#if EZ_EXP != 2 && EZ_EXP != 3
-                v = src >= 0 ? ld16v(out + src) : ld_clamped(out + src, out, out + cap);  // before the slot: zeros
-#else
-                v = V16{(uint64_t)src, h.lo};
-#endif
-            }
+            if (patt) v = pv;
 #if EZ_EXP != 1 && EZ_EXP != 3
             if (rem >= 16 || dst + 16 <= cap) st16v(out + dst, v);
             else put_small(out + dst, v, (uint32_t)rem);
 #else
             sinkv ^= v.lo;
 #endif
-            const int32_t k = rem < step ? rem : step;
-            dst += k;
-            src += k;
-            rem -= k;
+            const int32_t kk = rem < step ? rem : step;
+            dst += kk;
+            sp += kk;
+            rem -= kk;
         }
     }
 #if EZ_EXP == 1 || EZ_EXP == 3
