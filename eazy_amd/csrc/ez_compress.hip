@@ -25,6 +25,8 @@
 // reproduces block[x & mask] exactly:
 //   q = w.pos - bs + ((x - w.pos) mod bs);  byte = q >= start ? p[q-start]
 //                                                  : (ring ? ring[q & mask] : 0)
+#include <string>
+
 #include "ez_format.h"
 #include "ez_internal.h"
 #include "ez_wave.h"
@@ -419,14 +421,17 @@ uint64_t compress_scratch_words(const CompressArgs &a) {
     return grid * (uint64_t)a.hs;
 }
 
-// K1 variant choice: EZ_K1=lane|g16|wave|general overrides (A/B measurement)
+// K1 variant choice: EZ_K1=lane|g16|grp|wave|general overrides (A/B measurement)
 char compress_variant(const CompressArgs &a) {
     static int forced = -1;
     if (forced < 0) {
         const char *e = getenv("EZ_K1");
-        forced = !e ? 0 : (e[0] == 'l' ? 'l' : e[0] == 'g' && e[1] == '1' ? 'g' : e[0] == 'w' ? 'f' : e[0] == 'g' ? 'w' : 0);
+        const std::string v = e ? e : "";
+        forced = v == "lane" ? 'l' : v == "g16" ? 'g' : v == "grp" ? 'r' : v == "wave" ? 'f' : v == "general" ? 'w' : 0;
     }
     const bool lane = lane_scratch_halves(a) != 0, g16 = g16_stride_words(a) != 0, fresh = fresh_stride_words(a, 64) != 0;
+    const bool grp = grp_stride_words(a) != 0;
+    if (forced == 'r' && grp) return 'r';
     if (forced == 'l' && lane) return 'l';
     if (forced == 'g' && g16) return 'g';
     if (forced == 'f' && fresh) return 'f';
@@ -442,6 +447,7 @@ hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     const char v = compress_variant(a);
     if (v == 'l') return launch_compress_lane(a, (uint16_t *)a.ht_global, st);
     if (v == 'g') return launch_compress_g16(a, st);
+    if (v == 'r') return launch_compress_grp(a, st);
     if (v == 'f') return launch_compress_fresh(a, st, 64);
     const bool htl = a.hs <= kHtLdsMax;
     const bool pl = a.max_len > 0 && (int64_t)a.max_len <= kPLdsMax;

@@ -71,6 +71,8 @@ hipError_t launch_compress(const CompressArgs &a, hipStream_t s);
 uint32_t fresh_stride_words(const CompressArgs &a, int G);
 hipError_t launch_compress_fresh(const CompressArgs &a, hipStream_t s, int G);
 // K1l: fresh streams, one lane per stream (ez_compress_lane.hip); u16 scratch count*hs
+uint32_t grp_stride_words(const CompressArgs &a);
+hipError_t launch_compress_grp(const CompressArgs &a, hipStream_t s);
 uint64_t lane_scratch_halves(const CompressArgs &a);
 hipError_t launch_compress_lane(const CompressArgs &a, uint16_t *scratch, hipStream_t s);
 // the K1 variant a batch launch takes: 'l' lane, 'g' g16, 'f' fresh wave, 'w' general wave
