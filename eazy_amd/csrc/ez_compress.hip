@@ -436,6 +436,7 @@ char compress_variant(const CompressArgs &a) {
     if (forced == 'g' && g16) return 'g';
     if (forced == 'f' && fresh) return 'f';
     if (forced == 'w') return 'w';
+    if (grp) return 'r';  // fresh streams: G lanes per stream, LDS-staged (fastest at C1)
     if (lane && a.count >= 16384) return 'l';  // enough streams to fill the chip one lane each
     if (g16) return 'g';
     if (fresh) return 'f';

@@ -228,6 +228,7 @@ __global__ __launch_bounds__(64) void k1_grp(CompressArgs A, uint32_t stride_wor
         // ---- 2. capped judgement (exact decision)
         bool acc = false;
         uint64_t pcb = 0, pcf = 0;
+        int32_t known = 0;  // capped counts already exact below 8: forward | backward << 8
         if (valid) {
             P.around(cand, pcb, pcf);
             const bool rl = cand >= done && cand < x;
@@ -238,6 +239,10 @@ __global__ __launch_bounds__(64) void k1_grp(CompressArgs A, uint32_t stride_wor
             int32_t jf = ctz_bytes(pxf ^ (rl ? pcf : low_bytes(pcf, done - cand)));
             jf = jf < n - x ? jf : n - x;
             acc = rl ? (zr || jf + jb >= kMinCopyChunk) : ((jf < done - cand ? jf : done - cand) + jb >= kMinCopyChunk);
+            // zeros: 8 known zero bytes from the candidate, and the zero bytes before it (>= done)
+            int32_t zb = clz_bytes(pcb);
+            zb = zb < cand - done ? zb : cand - done;
+            known = zr ? (8 | (zb << 8)) : (jf | (jb << 8));
         }
         const uint32_t am = gball<G>(acc, g);
         const int a = am ? __builtin_ctz(am) : -1;  // the group's first accepting lane
@@ -259,10 +264,14 @@ __global__ __launch_bounds__(64) void k1_grp(CompressArgs A, uint32_t stride_wor
         const int mode = zr ? 0 : (rl ? 1 : 2);
         // forward from fa (zeros: from the candidate, 8 known zero bytes)
         const int32_t fa = zr ? ca : xa;
-        const int32_t f = gcount<G, true>(P, act, g, lj, fa, ca, mode, done, 0, n - fa);
+        const int32_t kn = bcast(known, src), fk = kn & 0xff, bk8 = kn >> 8;
+        // only a saturated capped count (8) needs the cooperative extension
+        const int32_t fx = gcount<G, true>(P, act && fk == 8, g, lj, fa, ca, mode, done, 8, n - fa);
+        const int32_t f = fk == 8 ? fx : fk;
         // backward before fa; window: the candidate side is below done
         const int32_t blim = zr ? ca - done : (rl ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
-        const int32_t c = gcount<G, false>(P, act, g, lj, fa, ca, mode, done, 0, blim);
+        const int32_t cx = gcount<G, false>(P, act && bk8 == 8, g, lj, fa, ca, mode, done, 8, blim);
+        const int32_t c = bk8 == 8 ? cx : bk8;
         if (act) {
             int32_t lit_end, nxt, clen;
             if (zr) {
