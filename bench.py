@@ -234,9 +234,10 @@ def main():
     if args.traffic_json and os.path.exists(args.traffic_json):
         # PMC pass of the same command (tools/traffic.py): HBM bytes per launch of the dominant kernel
         t = json.load(open(args.traffic_json))
-        names = {"k1_compress": ("k1_lane", "k1_g16", "k1_fresh", "k1_compress"), "k2_decompress": ("k2_fast",),
-                 "k3_pack": ("k3_gather",)}[dom]
-        traffic = next((t[n]["traffic"] for n in names if n in t and t[n]["traffic"]), None)
+        pre = {"k1_compress": "k1_", "k2_decompress": "k2_", "k3_pack": "k3_"}[dom]
+        # kernels of this step in the PMC pass: the launch's traffic = sum over its kernels (K2: fast + exact)
+        vals = [v["traffic"] for k, v in t.items() if k.startswith(pre) and v.get("traffic")]
+        traffic = sum(vals) if vals else None
 
     res = {
         "metric": "device-resident compress+decompress GiB/s, 1 MiB block",
