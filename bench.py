@@ -118,7 +118,7 @@ def e2e(ez, data, off, cb, packed, poff, ws, dws, out, osz, ost, block, htable, 
 
     def decomp():
         d_packed[:comp_bytes].copy_(h_packed, non_blocking=True)
-        ez.decompress_batch(d_packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws)
+        ez.decompress_batch(d_packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws, max_len=size)
         h_out.copy_(out[:total], non_blocking=True)
 
     t = {}
@@ -192,7 +192,7 @@ def main():
         ez.pack(cb, packed, poff, ws)
         if ev:
             ev[2].record()
-        ez.decompress_batch(packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws)
+        ez.decompress_batch(packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws, max_len=size)
         if ev:
             ev[3].record()
 

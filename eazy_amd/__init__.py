@@ -486,7 +486,7 @@ def pack(cb: CompressedBatch, packed=None, packed_off=None, workspace=None, stre
 
 
 def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=None, sizes=None, status=None,
-                     workspace=None, exact_only: bool = False, stream=None):
+                     workspace=None, exact_only: bool = False, stream=None, max_len: int = 0):
     """K2: decode complete streams comp[comp_off[s]:comp_off[s+1]] into
     out[out_off[s]:out_off[s+1]] -> (out, sizes, status).  exact_only skips
     the lane-per-stream fast decoder (every stream on the exact decoder)."""
@@ -504,7 +504,7 @@ def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=Non
     if workspace is None and not exact_only:
         workspace = torch.empty(_lib().ez_decompress_workspace(count), dtype=torch.uint8, device=dev)
     b = _Batch(comp.data_ptr(), comp_off.data_ptr(), out.data_ptr(), out_off.data_ptr(), sizes.data_ptr(),
-               status.data_ptr(), count, 0)
+               status.data_ptr(), count, max_len)
     ws = None if exact_only else workspace.data_ptr()
     _check(_lib().ez_decompress_batch(block_size_limit, C.byref(b), ws, _stream_ptr(stream)))
     return out, sizes, status

@@ -522,6 +522,7 @@ extern "C" int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, 
     a.block_size_limit = block_size_limit;
     a.handle = 0;
     a.slow = (uint32_t *)workspace;
+    a.max_out = b->max_len;  // decompress: the largest output slot, if the caller knows it
     EZ_HIP(ez::launch_decompress(a, (hipStream_t)hip_stream));
     return EZ_OK;
 }

@@ -61,6 +61,7 @@ struct DecompressArgs {
     int64_t boff;             // handle: absolute offset of in[0]
     DecodeState *st;          // handle: state in/out
     uint32_t *slow;           // batch: [0] = count, [1..] = streams the fast path handed over (nullptr = exact path only)
+    uint64_t max_out;         // batch: host hint, largest output slot (0 = unknown)
 };
 
 // words of workspace the two-level batch decoder needs

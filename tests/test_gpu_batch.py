@@ -27,10 +27,14 @@ def _run(cuda, bufs, block=MiB, htable=1024, magic=True):
     packed, poff = ez.pack(cb)
     out, sizes, status = ez.decompress_batch(packed, poff, off)
     out2, sizes2, status2 = ez.decompress_batch(packed, poff, off, exact_only=True)
+    mx = int(lens.max()) if len(lens) else 0
+    out3, sizes3, status3 = ez.decompress_batch(packed, poff, off, max_len=mx)
     torch.cuda.synchronize()
-    # the lane-per-stream fast decoder and the exact decoder agree
+    # the lane-per-stream fast decoder, the LDS group decoder and the exact decoder agree
     assert torch.equal(status, status2) and torch.equal(sizes, sizes2)
     assert torch.equal(out[: int(offs[-1])], out2[: int(offs[-1])])
+    assert torch.equal(status3, status2) and torch.equal(sizes3, sizes2)
+    assert torch.equal(out3[: int(offs[-1])], out2[: int(offs[-1])])
     return cb, packed.cpu().numpy(), poff.cpu().numpy(), out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy(), offs
 
 
