@@ -128,6 +128,17 @@ def device_count() -> int:
     return _lib().ez_device_count()
 
 
+def compress_kernel(block: int, htable: int, max_len: int, count: int) -> str:
+    """The K1 kernel a batch of `count` fresh streams of <= max_len bytes runs
+    on the current device ('t' tile, 'r' grp, 'l' lane, ...)."""
+    L = _lib()
+    L.ez_compress_kernel.argtypes = [C.c_int64, C.c_int64, C.c_uint64, C.c_uint64]
+    v = L.ez_compress_kernel(block, htable, max_len, count)
+    if v < 0:
+        _check(-v)
+    return chr(v)
+
+
 def _check(code: int, detail: int = 0) -> None:
     if code == OK:
         return

@@ -505,6 +505,19 @@ extern "C" int ez_pack_batch(const uint8_t *slots, const uint64_t *slot_off, con
     return EZ_OK;
 }
 
+extern "C" int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t count) {
+    if (!valid_writer_sizes(block, htable)) return -EZ_EINVAL;
+    if (device_count() <= 0) return -EZ_EDEVICE;
+    ez::CompressArgs a{};
+    a.count = count;
+    a.bs = block;
+    a.hs = htable;
+    a.max_len = max_len;
+    a.append_magic = 1;
+    a.header = 1;
+    return (int)ez::compress_variant(a);
+}
+
 extern "C" size_t ez_decompress_workspace(uint64_t count) {
     return (size_t)ez::decompress_workspace_words(count) * sizeof(uint32_t);
 }

@@ -421,21 +421,23 @@ uint64_t compress_scratch_words(const CompressArgs &a) {
     return grid * (uint64_t)a.hs;
 }
 
-// K1 variant choice: EZ_K1=lane|g16|grp|wave|general overrides (A/B measurement)
+// K1 variant choice: EZ_K1=lane|g16|grp|tile|wave|general overrides (A/B measurement)
 char compress_variant(const CompressArgs &a) {
     static int forced = -1;
     if (forced < 0) {
         const char *e = getenv("EZ_K1");
         const std::string v = e ? e : "";
-        forced = v == "lane" ? 'l' : v == "g16" ? 'g' : v == "grp" ? 'r' : v == "wave" ? 'f' : v == "general" ? 'w' : 0;
+        forced = v == "lane" ? 'l' : v == "g16" ? 'g' : v == "grp" ? 'r' : v == "tile" ? 't' : v == "wave" ? 'f' : v == "general" ? 'w' : 0;
     }
     const bool lane = lane_scratch_halves(a) != 0, g16 = g16_stride_words(a) != 0, fresh = fresh_stride_words(a, 64) != 0;
-    const bool grp = grp_stride_words(a) != 0;
+    const bool grp = grp_stride_words(a) != 0, tile = tile_stride_words(a) != 0;
+    if (forced == 't' && tile) return 't';
     if (forced == 'r' && grp) return 'r';
     if (forced == 'l' && lane) return 'l';
     if (forced == 'g' && g16) return 'g';
     if (forced == 'f' && fresh) return 'f';
     if (forced == 'w') return 'w';
+    if (tile) return 't';  // fresh streams: G lanes per stream, one exchange per window
     if (grp) return 'r';  // fresh streams: G lanes per stream, LDS-staged (fastest at C1)
     if (lane && a.count >= 16384) return 'l';  // enough streams to fill the chip one lane each
     if (g16) return 'g';
@@ -448,6 +450,7 @@ hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     const char v = compress_variant(a);
     if (v == 'l') return launch_compress_lane(a, (uint16_t *)a.ht_global, st);
     if (v == 'g') return launch_compress_g16(a, st);
+    if (v == 't') return launch_compress_tile(a, st);
     if (v == 'r') return launch_compress_grp(a, st);
     if (v == 'f') return launch_compress_fresh(a, st, 64);
     const bool htl = a.hs <= kHtLdsMax;

@@ -16,6 +16,8 @@
 #include "ez_wave.h"
 #include "ez_bytes.h"
 
+#include <string.h>
+
 namespace ez {
 namespace {
 
@@ -397,6 +399,16 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     }
     hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
+    // EZ_K2=grp: the LDS-resident group decoder (ez_decompress_grp.hip) for small streams
+    static const bool use_grp = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "grp") == 0;
+    const uint32_t R = use_grp ? grp_decode_region(a.max_out) : 0;
+    if (R) {
+        e = launch_decompress_grp(a, R, st);
+        if (e != hipSuccess) return e;
+        uint64_t grid = a.count < 4096 ? a.count : 4096;
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+        return hipGetLastError();
+    }
     static const unsigned blk = getenv("EZ_K2_BLOCK") ? (unsigned)atoi(getenv("EZ_K2_BLOCK")) : 256u;
     static const uint64_t maxw = getenv("EZ_K2_WAVES") ? (uint64_t)atoll(getenv("EZ_K2_WAVES")) : 0;
     uint64_t fgrid = (a.count + blk - 1) / blk;

@@ -76,6 +76,10 @@ uint32_t grp_stride_words(const CompressArgs &a);
 hipError_t launch_compress_grp(const CompressArgs &a, hipStream_t s);
 uint64_t lane_scratch_halves(const CompressArgs &a);
 hipError_t launch_compress_lane(const CompressArgs &a, uint16_t *scratch, hipStream_t s);
+// K1t: fresh streams, G lanes per stream, exchange-based visits (ez_compress_tile.hip)
+uint32_t tile_stride_words(const CompressArgs &a);
+bool lds_exchange_in_lane_order();  // the hardware property K1t relies on (checked once)
+hipError_t launch_compress_tile(const CompressArgs &a, hipStream_t s);
 // the K1 variant a batch launch takes: 'l' lane, 'g' g16, 'f' fresh wave, 'w' general wave
 char compress_variant(const CompressArgs &a);
 // K1g: fresh streams, 16 lanes per stream (ez_compress_g16.hip)
@@ -84,6 +88,9 @@ hipError_t launch_compress_g16(const CompressArgs &a, hipStream_t s);
 // u32 words of global hash-table scratch a batch launch needs (hs too big for LDS)
 uint64_t compress_scratch_words(const CompressArgs &a);
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t s);
+// K2grp: LDS region per stream for streams of <= max_out output bytes (0 = not usable)
+uint32_t grp_decode_region(uint64_t max_out);
+hipError_t launch_decompress_grp(const DecompressArgs &a, uint32_t R, hipStream_t s);
 hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
                        uint8_t *packed, uint64_t *packed_off, void *workspace, hipStream_t s);
 size_t pack_workspace(uint64_t count);

@@ -157,6 +157,12 @@ int ez_pack_batch(const uint8_t *slots, const uint64_t *slot_off, const uint64_t
 size_t ez_decompress_workspace(uint64_t count);
 int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *workspace, void *hip_stream);
 
+/* Introspection (no reference counterpart): the K1 kernel a batch of `count`
+ * fresh streams of <= max_len bytes would run on the current device, as a
+ * character: 't' tile (exchange visits), 'r' grp, 'l' lane, 'g' g16,
+ * 'f' fresh wave, 'w' general wave; EZ_EDEVICE (negated) without a device. */
+int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -131,3 +131,14 @@ def test_larger_than_window(cuda):
         bufs.append((b"abcdefgh" * 600)[:4000] + bytes(rng.integers(0, 256, 3000, dtype=np.uint8)))
     _check(cuda, bufs, 1024, 512)
     _check(cuda, bufs, 1024, 32)
+
+
+def test_tile_kernel_selected(cuda):
+    """The C1 shape runs K1t, whose visits rely on same-address LDS exchanges
+    applying in ascending lane order: the library checks that on the device
+    (tools/mb_ldsatomic.hip shows the measurement) and would fall back to
+    K1grp if it failed, so 't' here means the property holds on this GPU."""
+    import eazy_amd as ez
+
+    assert ez.compress_kernel(MiB, 1024, 4096, 65536) == "t"
+    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) != "t"  # 2n > block: the general kernel

@@ -119,6 +119,57 @@ def test_batch_decoder_errors_match_oracle(cuda):
     torch.cuda.synchronize()
     for out, sizes, status in res:
         _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
+    # the LDS group decoder (K2grp, taken when the largest slot is small) on the same corpus
+    cap = 8192
+    ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
+    out, sizes, status = ez.decompress_batch(comp, coff, ooff, max_len=cap)
+    torch.cuda.synchronize()
+    _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
+
+
+def test_batch_decoders_on_damaged_streams(cuda):
+    """Valid streams truncated, bit-flipped, padded, with breaks and with a
+    second header (MetaReset mid-stream): the group, lane and exact decoders
+    all give the oracle's bytes and first error."""
+    import torch
+
+    import eazy_amd as ez
+    import oracle as orc
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(21)
+    d = synth.logs(23, 48 * 4096).tobytes()
+    good = [orc.compress(1 << 20, 1024, [d[k * 4096 : (k + 1) * 4096]]) for k in range(48)]
+    ins = []
+    for k, c in enumerate(good):
+        c = bytearray(c)
+        kind = k % 8
+        if kind == 0:
+            c = c[: int(rng.integers(1, len(c)))]
+        elif kind == 1:
+            for _ in range(3):
+                c[int(rng.integers(0, len(c)))] ^= 1 << int(rng.integers(0, 8))
+        elif kind == 2:
+            at = int(rng.integers(9, len(c)))
+            c = c[:at] + bytes(int(rng.integers(1, 20))) + c[at:]
+        elif kind == 3:
+            c = c + b"\x80\x1f" + bytes(3)
+        elif kind == 4:
+            c = c + good[(k + 1) % len(good)]
+        elif kind == 5:
+            c = c[:9] + b"\x80\x1f" + c[9:]
+        elif kind == 6:
+            c = c[:3] + c[9:]  # no magic meta: the reset meta alone
+        ins.append(bytes(c))
+    offs = np.concatenate([[0], np.cumsum([len(b) for b in ins])]).astype(np.int64)
+    comp = torch.from_numpy(np.frombuffer(b"".join(ins), np.uint8).copy()).to(cuda)
+    coff = torch.from_numpy(offs).to(cuda)
+    for cap in (4096, 8192):
+        ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
+        for kw in ({"max_len": cap}, {}, {"exact_only": True}):
+            out, sizes, status = ez.decompress_batch(comp, coff, ooff, **kw)
+            torch.cuda.synchronize()
+            _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
 
 
 def _cmp_oracle(ins, cap, out, sizes, status):
