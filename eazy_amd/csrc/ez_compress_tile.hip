@@ -40,6 +40,29 @@ namespace ez {
 namespace {
 using namespace k1;
 
+// EZ_EXP bit 2: cycle profile of the window loop (s_memtime between section
+// marks, printed by lane 0 of the first blocks); diagnostic builds only
+#if (EZ_EXP & 4)
+#define EZ_PROF_MARK(k)                                            \
+    do {                                                           \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime();          \
+        prof[(k) == 0 ? 7 : (k) - 1] += t_ - prof_t;               \
+        prof_t = t_;                                               \
+        if ((k) == 0) prof_it++;                                   \
+    } while (0)
+#define EZ_PROF_DUMP()                                                                                         \
+    do {                                                                                                       \
+        if (blockIdx.x < 3 && lane == 0)                                                                       \
+            printf("prof blk %u it %llu: visit %llu judge %llu ballot %llu ext %llu enc %llu emit %llu fin %llu loop %llu\n", \
+                   blockIdx.x, (unsigned long long)prof_it, (unsigned long long)prof[0], (unsigned long long)prof[1], \
+                   (unsigned long long)prof[2], (unsigned long long)prof[3], (unsigned long long)prof[4],            \
+                   (unsigned long long)prof[5], (unsigned long long)prof[6], (unsigned long long)prof[7]);           \
+    } while (0)
+#else
+#define EZ_PROF_MARK(k) do {} while (0)
+#define EZ_PROF_DUMP() do {} while (0)
+#endif
+
 typedef uint32_t __attribute__((aligned(1))) u32_ua;
 
 // bytes [k, k+4) of the 16-byte little-endian value (lo, hi), 0 <= k <= 12
@@ -150,6 +173,9 @@ __global__ __launch_bounds__(64) void k1_tile(CompressArgs A, uint32_t stride_wo
     int32_t i = 0, done = 0, hiw = -1;  // hiw: highest position in the table
     bool live = have && n >= 4 && !err;
     int32_t guard = 4 * n + 64;
+#if (EZ_EXP & 4)
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime(), prof_it = 0;
+#endif
     while (__ballot(live) != 0) {
         if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
         int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
@@ -157,6 +183,7 @@ __global__ __launch_bounds__(64) void k1_tile(CompressArgs A, uint32_t stride_wo
         const int32_t x = i + lj;
         const bool valid = live && lj < nvalid;
 
+        EZ_PROF_MARK(0);
         // ---- 1. visit: hash, exchange (lookup + insert in lane order)
         uint64_t pxb = 0, pxf = 0;
         uint32_t h = 0;
@@ -167,6 +194,7 @@ __global__ __launch_bounds__(64) void k1_tile(CompressArgs A, uint32_t stride_wo
             cand = (int32_t)atomicExch(&ht[h], (uint32_t)x);
         }
 
+        EZ_PROF_MARK(1);
         // ---- 2. capped judgement (exact decision)
         bool acc = false;
         int32_t info = 0;  // cand | forward count << 16 | backward count << 20 | rl << 24 | zr << 25
@@ -186,6 +214,7 @@ __global__ __launch_bounds__(64) void k1_tile(CompressArgs A, uint32_t stride_wo
             const int32_t fk = zr ? 8 : jf, bk = zr ? zb : jb;
             info = cand | (fk << 16) | (bk << 20) | ((int32_t)rl << 24) | ((int32_t)zr << 25);
         }
+        EZ_PROF_MARK(2);
         const uint32_t am = gball<G>(acc, g);
         const int a = am ? __builtin_ctz(am) : -1;  // the group's first accepting lane
 
@@ -201,11 +230,13 @@ __global__ __launch_bounds__(64) void k1_tile(CompressArgs A, uint32_t stride_wo
         const int mode = zr ? 0 : (rl ? 1 : 2);
         const int32_t fa = zr ? ca : xa;
         constexpr bool kExt = (EZ_EXP & 2) == 0;
+        EZ_PROF_MARK(3);
         const int32_t fx = gcount<G, true>(P, kExt && act && fk == 8, g, lj, fa, ca, mode, done, 8, n - fa);
         const int32_t f = fk == 8 ? fx : fk;
         const int32_t blim = zr ? ca - done : (rl ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
         const int32_t cx = gcount<G, false>(P, kExt && act && bk8 == 8, g, lj, fa, ca, mode, done, 8, blim);
         const int32_t c = bk8 == 8 ? cx : bk8;
+        EZ_PROF_MARK(4);
         int32_t lit_end = 0, nxt = 0, clen = 0, T = 0, e1 = 0, e2 = 0;
         uint64_t lb = 0, cb = 0, ch2 = 0;
         if (act) {
@@ -240,8 +271,10 @@ __global__ __launch_bounds__(64) void k1_tile(CompressArgs A, uint32_t stride_wo
             T = e2 + tn + on;
             if (op + T > cap) err = EZ_ENOSPC;
         }
+        EZ_PROF_MARK(5);
         const bool wr = act && !err && (EZ_EXP & 1) == 0;
         emit<G, SRC>(P, out, op, cap, wr, lj, T, e1, e2, lb, done, cb, ch2);
+        EZ_PROF_MARK(6);
         if (act) {
             // the extra insert of i+1 after a window match (writer.go:315-318)
             if (!rl && xa + 1 + 4 <= n && lj == 0) {
@@ -258,6 +291,7 @@ __global__ __launch_bounds__(64) void k1_tile(CompressArgs A, uint32_t stride_wo
             i += nvalid;
         }
         if (live && (err || i + 4 > n)) live = false;
+        EZ_PROF_MARK(7);
 
     }
     // trailing literal (writer.go:324-329)
@@ -273,6 +307,7 @@ __global__ __launch_bounds__(64) void k1_tile(CompressArgs A, uint32_t stride_wo
         emit<G, SRC>(P, out, op, cap, tail && !err && (EZ_EXP & 1) == 0, lj, T, ln, T, lb, done, 0, 0);
         if (tail && !err) op += T;
     }
+    EZ_PROF_DUMP();
     if (have && lj == 0) {
         A.out_size[s] = (uint64_t)op;
         if (A.status) A.status[s] = err;

@@ -397,6 +397,14 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
         return hipGetLastError();
     }
+    static const bool use_exact = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "exact") == 0;
+    if (use_exact) {
+        DecompressArgs b = a;
+        b.slow = nullptr;
+        uint64_t grid = b.count < (1u << 30) ? b.count : (1u << 30);
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, b);
+        return hipGetLastError();
+    }
     hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // EZ_K2=grp: the LDS-resident group decoder (ez_decompress_grp.hip) for small streams
