@@ -139,6 +139,12 @@ def compress_kernel(block: int, htable: int, max_len: int, count: int) -> str:
     return chr(v)
 
 
+def select_compress_kernel(kind: str = "") -> None:
+    """Force the K1 kernel of later batch calls ('s', 'S', 't', ...; '' =
+    automatic).  Tests and A/B measurement only."""
+    _check(_lib().ez_select_compress_kernel(ord(kind) if kind else 0))
+
+
 def _check(code: int, detail: int = 0) -> None:
     if code == OK:
         return

@@ -518,6 +518,13 @@ extern "C" int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_le
     return (int)ez::compress_variant(a);
 }
 
+extern "C" int ez_select_compress_kernel(int kind) {
+    if (kind != 0 && !strchr("sStrlgfw", kind)) return EZ_EINVAL;
+    ez::select_split_table(kind == 'S');
+    ez::select_compress_variant(kind == 'S' ? 's' : kind);
+    return EZ_OK;
+}
+
 extern "C" size_t ez_decompress_workspace(uint64_t count) {
     return (size_t)ez::decompress_workspace_words(count) * sizeof(uint32_t);
 }

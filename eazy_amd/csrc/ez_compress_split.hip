@@ -1,0 +1,569 @@
+// ez_compress_split.hip — K1s: batch compression of fresh streams in two
+// kernels, the greedy parse (K1p) and the token writer (K1e).
+//
+// Writer.Write (writer.go:206-337) for a fresh stream (SURVEY §8 unit of
+// work; 2n <= block, so the ring is the linear history with zeros from `done`
+// on: no far skip, no cut, no trim 1).
+//
+// Why two kernels.  The parse is a serial chain per stream: every window's
+// decision needs the table after the previous one.  Writing the tokens
+// (Encoder.Tag/Offset :537-597, appendLiteral/appendCopy :519-527) does not
+// feed back into that chain, but done inside it (K1t) it puts the literal
+// loads, the encodes and the stores on every iteration's critical path.  Here
+//   K1p (G lanes per stream, the table in LDS) runs only the chain: visit,
+//       capped judgement, exact extension of an accepted match, the i+1
+//       insert, and one 16-byte match record per accepted match
+//       {lit_end, copy length, distance, flags} into a per-stream record slot;
+//   K1e (one wave per stream) turns the records into the byte stream: token
+//       sizes, a wave prefix sum for their output positions, then every lane
+//       writes its token (literal tag, literal bytes, copy tag + offset) with
+//       16-byte stores and exact-length tails; long literals are copied by the
+//       whole wave.  Streams whose tokens do not fit their slot stop at the
+//       last token that fits (EZ_ENOSPC), as the single-kernel path does.
+//
+// The window.  The G lanes of a stream judge positions i .. i+G-1 at once
+// against the table as Go's sequential visits (writer.go:213-217) would leave
+// it, and the first accepting lane wins.  Two ways to visit a window:
+//   T16 (u16 table, 2 bytes per entry, twice the streams per CU of T32):
+//       lanes read the table, a lane's candidate is the nearest earlier lane of
+//       the window with the same hash (DPP row shifts) or else the table value,
+//       and after the decision the lanes Go visits (those up to the accepting
+//       one) store their positions with one ds_write_b16, where same-address
+//       stores of one instruction land in ascending lane order (checked on the
+//       device once per process; T32 is used if it fails).  Exact for any
+//       table contents, so backward jumps need nothing special.
+//   T32 (u32 table): one ds_wrxchg_rtn_b32 visits the window in lane order,
+//       inserts of lanes Go does not visit are undone with one ds_min_u32,
+//       which needs inserts monotone in position: windows that start at or
+//       below the highest inserted position are judged one position at a time.
+// Acceptance is decided with 8-byte capped counts (minCopyChunk = 6 < 8,
+// writer.go:119, 301); only a saturated count is extended, forward and
+// backward at once, 16 bytes per lane.  Each accepted match advances `done` by
+// its copy length (>= 6), so a stream of n bytes makes at most n/6 records.
+#include "ez_format.h"
+#include "ez_internal.h"
+#include "ez_wave.h"
+#include "ez_k1_common.h"
+
+#ifndef EZ_EXP
+#define EZ_EXP 0  // diagnostic builds only: bit 2 = cycle profile of the parse loop
+#endif
+
+namespace ez {
+namespace {
+using namespace k1;
+
+#if (EZ_EXP & 4)
+#define EZ_PROF_MARK(k)                                   \
+    do {                                                  \
+        __builtin_amdgcn_s_waitcnt(0);                    \
+        const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+        prof[k] += t_ - prof_t;                           \
+        prof_t = t_;                                      \
+    } while (0)
+#else
+#define EZ_PROF_MARK(k) do {} while (0)
+#endif
+
+constexpr uint32_t kRecForce = 1;    // flags: literal emitted even when empty (writeRunlen :480)
+constexpr int64_t kMaxT16 = 65535;   // T16 positions fit 16 bits
+constexpr int64_t kMaxT32 = 1 << 19; // the judgement packs the candidate into 20 bits (and 2n <= block)
+
+// record slot of stream s: s * rec_cap .. ; rec_cap = max_len / 6 + 1
+__host__ __device__ __forceinline__ uint64_t rec_cap(uint64_t max_len) { return max_len / 6 + 1; }
+
+// bytes [0, k) of v kept, the rest 0 (k <= 0: none, k >= 16: all)
+__device__ __forceinline__ V16 keep_low16(V16 v, int32_t k) {
+    const uint64_t ml = k >= 8 ? ~0ull : (k <= 0 ? 0ull : (1ull << (8 * k)) - 1);
+    const uint64_t mh = k >= 16 ? ~0ull : (k <= 8 ? 0ull : (1ull << (8 * (k - 8))) - 1);
+    return V16{v.lo & ml, v.hi & mh};
+}
+
+// 16 bytes from y of the match's source side: mode 0 zeros (zero region),
+// 1 the stream itself (run length), 2 the ring image of a fresh window
+// (bytes before the stream start and from `done` on read 0)
+__device__ __forceinline__ V16 src16(const GW &P, int32_t y, int mode, int32_t done) {
+    if (mode == 0) return V16{0, 0};
+    uint64_t lo, hi;
+    P.around(y + 8, lo, hi);  // bytes y .. y+15, zeros before the stream start
+    const V16 v{lo, hi};
+    return mode == 2 ? keep_low16(v, done - y) : v;
+}
+
+// Exact forward and backward match counts of one group at once, past the 8
+// bytes the capped judgement already compared: lanes 0..G/2-1 scan forward
+// (a+k vs b+k), lanes G/2..G-1 backward (a-1-k vs b-1-k), 16 bytes per lane
+// per step, so a count below 8 + 8G bytes costs one load round trip.
+template <int G>
+__device__ __forceinline__ void gext(const GW &P, bool runf, bool runb, int g, int lj, int32_t a, int32_t b, int mode,
+                                     int32_t done, int32_t limf, int32_t limb, int32_t &resf, int32_t &resb) {
+    constexpr int H = G / 2;
+    constexpr uint32_t kHalf = (1u << H) - 1;
+    const bool fw = lj < H;
+    const int t = lj % H;
+    resf = 8 < limf ? 8 : limf;
+    resb = 8 < limb ? 8 : limb;
+    bool gof = runf && 8 < limf, gob = runb && 8 < limb;
+    int32_t basef = 8, baseb = 8;
+    while (__ballot(gof || gob) != 0) {
+        const bool mine = fw ? gof : gob;
+        const int32_t lim = fw ? limf : limb;
+        const int32_t k = (fw ? basef : baseb) + 16 * t;
+        int32_t mb = 16;
+        if (mine) {
+            if (k < lim) {
+                const int32_t ya = fw ? a + k : a - k - 16, yb = fw ? b + k : b - k - 16;
+                uint64_t alo, ahi;
+                P.around(ya + 8, alo, ahi);
+                const V16 vb = src16(P, yb, mode, done);
+                const uint64_t dl = alo ^ vb.lo, dh = ahi ^ vb.hi;
+                if (fw) mb = dl ? (int32_t)(__builtin_ctzll(dl) >> 3) : (dh ? 8 + (int32_t)(__builtin_ctzll(dh) >> 3) : 16);
+                else mb = dh ? (int32_t)(__builtin_clzll(dh) >> 3) : (dl ? 8 + (int32_t)(__builtin_clzll(dl) >> 3) : 16);
+                if (mb > lim - k) mb = lim - k;
+            } else {
+                mb = 0;
+            }
+        }
+        const uint32_t bad = gball<G>(mine && mb < 16, g);
+        const uint32_t bf = bad & kHalf, bb = bad >> H;
+        const int lf = bf ? __builtin_ctz(bf) : 0, lb = bb ? __builtin_ctz(bb) : 0;
+        const int32_t mbf = bcast(mb, G * g + lf), mbb = bcast(mb, G * g + H + lb);
+        if (gof) {
+            if (bf) {
+                resf = basef + 16 * lf + mbf;
+                resf = resf < limf ? resf : limf;
+                gof = false;
+            } else {
+                basef += 16 * H;
+                if (basef >= limf) { resf = limf; gof = false; }
+            }
+        }
+        if (gob) {
+            if (bb) {
+                resb = baseb + 16 * lb + mbb;
+                resb = resb < limb ? resb : limb;
+                gob = false;
+            } else {
+                baseb += 16 * H;
+                if (baseb >= limb) { resb = limb; gob = false; }
+            }
+        }
+    }
+}
+
+// v of the lane K below in the same 16-lane row (~0u where there is none)
+template <int K>
+__device__ __forceinline__ uint32_t row_shr(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)~0u, (int)v, 0x110 + K, 0xf, 0xf, false);
+}
+// distance to the nearest earlier lane of the group with the same hash (0: none)
+template <int K>
+struct Pred {
+    __device__ __forceinline__ static int32_t get(uint32_t h, int lj, int32_t d) {
+        const uint32_t hk = row_shr<K>(h);
+        d = (K <= lj && hk == h) ? K : d;  // descending K: the nearest one stays
+        return Pred<K - 1>::get(h, lj, d);
+    }
+};
+template <>
+struct Pred<0> {
+    __device__ __forceinline__ static int32_t get(uint32_t, int, int32_t d) { return d; }
+};
+
+// ---------------------------------------------------------------- K1p
+template <int G, bool T16>
+__global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_words, uint4 *recs, uint64_t rcap) {
+    constexpr int S = 64 / G;
+    static_assert(!T16 || G <= 16, "T16 predecessor search works within 16-lane DPP rows");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = (int)(threadIdx.x & 63);
+    const int g = lane / G, lj = lane % G;
+    const int32_t hs = (int32_t)A.hs;
+    const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(hs - 1)));
+    uint32_t *htw = (uint32_t *)smem + (uint32_t)g * stride_words;
+    uint16_t *hth = (uint16_t *)htw;
+
+    const uint64_t s = (uint64_t)blockIdx.x * S + g;
+    const bool have = s < A.count;
+    int32_t n = 0;
+    const uint8_t *gp = A.in;
+    if (have) {
+        n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+        gp = A.in + A.in_off[s];
+    }
+    GW P;
+    P.p = gp;
+    P.blo = A.in;
+    P.bhi = A.in + A.in_off[A.count];
+    uint4 *rec = recs + (have ? s * rcap : 0);
+    // ht zero = stream position 0 (writer.go:183, A.2)
+    for (int32_t k = 4 * lj; k < (int32_t)stride_words; k += 4 * G) *(uint4 *)(htw + k) = make_uint4(0, 0, 0, 0);
+
+    // the launcher sized records and tables from max_len: longer streams are refused
+    int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : 0;
+    int32_t i = 0, done = 0, hiw = -1, nrec = 0;  // hiw: highest position in the table (T32)
+    bool live = have && n >= 4 && !err;
+    int32_t guard = 4 * n + 64;
+    uint64_t pxb = 0, pxf = 0;  // bytes before / from this lane's position (loaded one window ahead)
+    if (live) P.around(i + lj, pxb, pxf);
+#if (EZ_EXP & 4)
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime(), prof_it = 0;
+#endif
+    while (__ballot(live) != 0) {
+#if (EZ_EXP & 4)
+        prof_it++;
+#endif
+        if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
+        int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
+        if (!T16 && i <= hiw) nvalid = 1;  // T32, not monotone: one position per window
+        const int32_t x = i + lj;
+        const bool valid = live && lj < nvalid;
+
+        // ---- visit: hash, lookup (+ insert for T32) in lane order, writer.go:213-217
+        const uint32_t h = valid ? ((uint32_t)pxf * kHashMul) >> hsh : 0u;
+        int32_t cand = 0;
+        if constexpr (T16) {
+            const int32_t tv = valid ? (int32_t)hth[h] : 0;
+            const int32_t d = Pred<G - 1>::get(h, lj, 0);
+            cand = d ? x - d : tv;
+        } else {
+            if (valid) cand = (int32_t)atomicExch(&htw[h], (uint32_t)x);
+        }
+        EZ_PROF_MARK(0);
+
+        // ---- capped judgement (exact decision), writer.go:219-301, writeRunlen :441-463
+        bool acc = false;
+        int32_t info = 0;  // cand | forward count << 20 | backward count << 24 | rl << 28 | zr << 29
+        uint64_t pcb = 0, pcf = 0;
+        if (valid) P.around(cand, pcb, pcf);
+        EZ_PROF_MARK(5);
+        if (valid) {
+            const bool rl = cand >= done && cand < x;
+            const bool zr = rl && cand + 8 < n && pcf == 0;
+            const int32_t bl = rl ? ((x - done) < cand ? (x - done) : cand) : x - done;
+            int32_t jb = clz_bytes(pxb ^ pcb);
+            jb = jb < bl ? jb : bl;
+            int32_t jf = ctz_bytes(pxf ^ (rl ? pcf : low_bytes(pcf, done - cand)));
+            jf = jf < n - x ? jf : n - x;
+            acc = rl ? (zr || jf + jb >= kMinCopyChunk) : ((jf < done - cand ? jf : done - cand) + jb >= kMinCopyChunk);
+            int32_t zb = clz_bytes(pcb);
+            zb = zb < cand - done ? zb : cand - done;
+            const int32_t fk = zr ? 8 : jf, bk = zr ? zb : jb;
+            info = cand | (fk << 20) | (bk << 24) | ((int32_t)rl << 28) | ((int32_t)zr << 29);
+        }
+        EZ_PROF_MARK(1);
+        const uint32_t am = gball<G>(acc, g);
+        const int a = am ? __builtin_ctz(am) : -1;  // the group's first accepting lane
+
+        // ---- T32: undo the inserts of the lanes Go does not visit
+        if constexpr (!T16) {
+            if (valid && a >= 0 && lj > a) atomicMin(&htw[h], (uint32_t)cand);
+        }
+
+        // ---- the accepted match: exact lengths (cooperative extension of saturated counts)
+        const int32_t ib = bcast(info, G * g + (a < 0 ? 0 : a));
+        // the hash of xa+1 is lane a+1's (when it visited), for the extra insert
+        const uint32_t h1v = (uint32_t)bcast((int32_t)h, G * g + (a + 1 < G ? a + 1 : G - 1));
+        const bool act = live && a >= 0;
+        const int32_t xa = i + a;
+        const int32_t ca = ib & 0xfffff, fk = (ib >> 20) & 0xf, bk8 = (ib >> 24) & 0xf;
+        const bool rl = (ib >> 28) & 1, zr = (ib >> 29) & 1;
+        const int mode = zr ? 0 : (rl ? 1 : 2);
+        const int32_t fa = zr ? ca : xa;
+        EZ_PROF_MARK(2);
+        const int32_t blim = zr ? ca - done : (rl ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
+        int32_t fx, cx;
+        gext<G>(P, act && fk == 8, act && bk8 == 8, g, lj, fa, ca, mode, done, n - fa, blim, fx, cx);
+        const int32_t f = fk == 8 ? fx : fk;
+        const int32_t c = bk8 == 8 ? cx : bk8;
+        EZ_PROF_MARK(3);
+        int32_t lit_end = 0, nxt = 0;
+        if (act) {
+            if (zr) {  // writeZeros :407-439
+                lit_end = ca - c;
+                nxt = ca + f;
+            } else if (rl) {  // writeRunlen :441-489
+                lit_end = xa - c;
+                nxt = xa + f;
+            } else {  // window match, trim 2 (:292-296)
+                const int32_t over = ca + f - done;
+                lit_end = xa - c;
+                nxt = xa + f - (over > 0 ? over : 0);
+            }
+            const int32_t top = rl ? xa : xa + 1;
+            hiw = hiw > top ? hiw : top;
+            i = done = nxt;
+        } else if (live) {
+            const int32_t top = i + nvalid - 1;
+            hiw = hiw > top ? hiw : top;
+            i += nvalid;
+        }
+        if (live && (err || i + 4 > n)) live = false;
+        // the next window's bytes, in flight while this window's table writes and record go out
+        EZ_PROF_MARK(6);
+        if (live) P.around(i + lj, pxb, pxf);
+        EZ_PROF_MARK(7);
+
+        // ---- T16: the lanes Go visits store their positions (the last of a hash wins)
+        if constexpr (T16) {
+            if (valid && (a < 0 || lj <= a)) hth[h] = (uint16_t)x;
+        }
+        if (act && lj == 0) {
+            if ((uint64_t)nrec < rcap)
+                rec[nrec] = make_uint4((uint32_t)lit_end, (uint32_t)(nxt - lit_end), (uint32_t)(zr ? 0 : xa - ca),
+                                       (rl && !zr) ? kRecForce : 0u);
+            // the extra insert of i+1 after a window match (writer.go:315-318)
+            if (!rl && xa + 1 + 4 <= n) {
+                const uint32_t h1 = a + 1 < nvalid ? h1v : ((P.u32(xa + 1) * kHashMul) >> hsh);
+                if constexpr (T16) hth[h1] = (uint16_t)(xa + 1);
+                else htw[h1] = (uint32_t)(xa + 1);
+            }
+        }
+        if (act) {
+            if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
+            nrec++;
+        }
+        EZ_PROF_MARK(4);
+    }
+#if (EZ_EXP & 4)
+    if (blockIdx.x < 4 && lane == 0)
+        printf("prof blk %u it %llu: visit %llu cload %llu judge %llu ballot %llu ext %llu upd %llu xload %llu fin %llu\n", blockIdx.x,
+               (unsigned long long)prof_it, (unsigned long long)prof[0], (unsigned long long)prof[5], (unsigned long long)prof[1],
+               (unsigned long long)prof[2], (unsigned long long)prof[3], (unsigned long long)prof[6], (unsigned long long)prof[7],
+               (unsigned long long)prof[4]);
+#endif
+    if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
+}
+
+// ---------------------------------------------------------------- K1e
+// 16 bytes at y of the batch [lo, hi) (bytes outside read as 0)
+__device__ __forceinline__ V16 ld16_in(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
+    return y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
+}
+
+// copy L bytes src -> dst, one lane
+__device__ __forceinline__ void copy_lane(uint8_t *dst, const uint8_t *src, int32_t L, const uint8_t *lo, const uint8_t *hi) {
+    int32_t q = 0;
+    for (; q + 16 <= L; q += 16) st16v(dst + q, ld16_in(src + q, lo, hi));
+    if (q < L) put_small(dst + q, ld16_in(src + q, lo, hi), (uint32_t)(L - q));
+}
+
+constexpr int32_t kLongLit = 96;  // literals this long are copied by the whole wave
+
+__global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint4 *recs, uint64_t rcap) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t s = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (s >= A.count) return;
+    const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
+    const uint8_t *p = A.in + A.in_off[s];
+    const int32_t n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+    uint8_t *out = A.out + A.out_off[s];
+    const int64_t cap64 = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    const int32_t cap = cap64 > 0x7fffffff ? 0x7fffffff : (int32_t)cap64;
+    const uint64_t pr = A.out_size[s];
+    const uint64_t m64 = pr & 0xffffffffffffull;
+    const int32_t m = (int32_t)(m64 < rcap ? m64 : rcap);
+    int err = (int)(pr >> 48);
+    const uint4 *rec = recs + s * rcap;
+
+    // header (writer.go:495-517): magic + reset, or reset alone
+    const int32_t H = A.append_magic ? 9 : 3;
+    if (H > cap) {
+        if (lane == 0) {
+            A.out_size[s] = 0;
+            if (A.status) A.status[s] = EZ_ENOSPC;
+        }
+        return;
+    }
+    if (lane == 0) {
+        const int32_t bsl = (int32_t)__builtin_ctzll((uint64_t)A.bs);
+        const uint64_t hm = A.append_magic ? (0x141080797a616502ull << 8 | 0x80) : (0x80ull | 0x10ull << 8 | (uint64_t)bsl << 16);
+        const V16 hv{hm, A.append_magic ? (uint64_t)bsl : 0ull};
+        put_small(out, hv, (uint32_t)H);
+    }
+    int32_t op = H, done = 0;
+    bool full = false;
+    for (int32_t b0 = 0; b0 < m && !full; b0 += 64) {
+        const int32_t k = b0 + lane;
+        const bool here = k < m;
+        const uint4 r = here ? rec[k] : make_uint4(0, 0, 0, 0);
+        const int32_t lit_end = (int32_t)r.x, clen = (int32_t)r.y, dist = (int32_t)r.z;
+        const int32_t end = lit_end + clen;
+        const int32_t prev = __shfl_up(end, 1, 64);
+        const int32_t dk = lane == 0 ? done : prev;
+        const int32_t L = lit_end - dk;
+        const bool lit = here && ((r.w & kRecForce) != 0 || L > 0);
+        int32_t ln = 0, tn = 0, on = 0;
+        const uint64_t lb = tag_bytes(0x00, L, &ln);
+        if (!lit) ln = 0;
+        const uint64_t tb = tag_bytes(0x80, clen, &tn);
+        const uint64_t ob = off_bytes(dist, clen, &on);
+        const int32_t T = here ? ln + (lit ? L : 0) + tn + on : 0;
+        // inclusive prefix sum of T over the wave
+        int32_t incl = T;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int32_t v = __shfl_up(incl, d, 64);
+            if (lane >= d) incl += v;
+        }
+        const int32_t tok = op + incl - T;  // this token's output position
+        const bool fits = here && tok + T <= cap;
+        const uint64_t nofit = __ballot(here && !fits);
+        const int lastok = nofit ? __builtin_ctzll(nofit) - 1 : 63;  // last lane whose token is written
+        const bool wr = fits && lane <= lastok;
+        bool longlit = false;
+        if (wr) {
+            uint8_t *d = out + tok;
+            if (ln) put_small(d, V16{lb, 0}, (uint32_t)ln);
+            if (lit) {
+                if (L >= kLongLit) longlit = true;
+                else copy_lane(d + ln, p + dk, L, lo, hi);
+            }
+            const uint64_t c0 = tb | (ob << (8 * tn));
+            const uint64_t c1 = ob >> (64 - 8 * tn);  // tn >= 1
+            put_small(d + T - tn - on, V16{c0, c1}, (uint32_t)(tn + on));
+        }
+        // long literals: the whole wave, one at a time
+        for (uint64_t lm = __ballot(longlit); lm; lm &= lm - 1) {
+            const int src = __builtin_ctzll(lm);
+            const int32_t Ls = __shfl(L, src, 64), ds = __shfl(dk, src, 64), ts = __shfl(tok, src, 64) + __shfl(ln, src, 64);
+            for (int32_t q = 16 * lane; q < Ls; q += 16 * 64) {
+                const V16 v = ld16_in(p + ds + q, lo, hi);
+                if (q + 16 <= Ls) st16v(out + ts + q, v);
+                else put_small(out + ts + q, v, (uint32_t)(Ls - q));
+            }
+        }
+        if (nofit) {
+            full = true;
+            err = err ? err : EZ_ENOSPC;
+            op = __shfl(tok, lastok + 1, 64);
+        } else {
+            op = __shfl(op + incl, 63, 64);
+            done = __shfl(end, (m - b0 >= 64 ? 63 : m - b0 - 1), 64);
+        }
+    }
+    // trailing literal (writer.go:324-329)
+    if (!full && !err && done < n) {
+        const int32_t L = n - done;
+        int32_t ln = 0;
+        const uint64_t lb = tag_bytes(0x00, L, &ln);
+        if (op + ln + L > cap) {
+            err = EZ_ENOSPC;
+        } else {
+            if (lane == 0) put_small(out + op, V16{lb, 0}, (uint32_t)ln);
+            const int32_t ts = op + ln;
+            for (int32_t q = 16 * lane; q < L; q += 16 * 64) {
+                const V16 v = ld16_in(p + done + q, lo, hi);
+                if (q + 16 <= L) st16v(out + ts + q, v);
+                else put_small(out + ts + q, v, (uint32_t)(L - q));
+            }
+            op += ln + L;
+        }
+    }
+    if (lane == 0) {
+        A.out_size[s] = (uint64_t)op;
+        if (A.status) A.status[s] = err;
+    }
+}
+
+// LDS words per stream (0 = this variant cannot take the batch)
+template <int G, bool T16>
+uint32_t split_stride(const CompressArgs &a) {
+    if (a.ring || a.max_len == 0 || 2 * (int64_t)a.max_len > a.bs || a.hs > 4096 || a.hs < 4) return 0;
+    if ((int64_t)a.max_len > (T16 ? kMaxT16 : kMaxT32)) return 0;
+    const uint64_t words = T16 ? ((uint64_t)a.hs + 1) / 2 : (uint64_t)a.hs;
+    const uint64_t w = (words + 3) & ~3ull;
+    if (w * 4 * (64 / G) > 160 * 1024) return 0;
+    return (uint32_t)w;
+}
+
+int split_g() {
+    static const int g = getenv("EZ_K1S_G") ? atoi(getenv("EZ_K1S_G")) : 16;
+    return g == 8 ? 8 : 16;
+}
+bool g_split_t32 = false;  // ez_select_compress_kernel('S')
+bool split_t32_forced() {
+    static const bool v = getenv("EZ_K1S_T") && atoi(getenv("EZ_K1S_T")) == 32;
+    return v || g_split_t32;
+}
+
+template <int G, bool T16>
+hipError_t launch_split_g(const CompressArgs &a, uint4 *recs, hipStream_t st) {
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void *)k1_parse<G, T16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_done = true;
+    }
+    constexpr int S = 64 / G;
+    const uint32_t stride = split_stride<G, T16>(a);
+    const uint64_t rcap = rec_cap(a.max_len);
+    const unsigned grid = (unsigned)((a.count + S - 1) / S);
+    hipLaunchKernelGGL((k1_parse<G, T16>), dim3(grid), dim3(64), (size_t)stride * 4 * S, st, a, stride, recs, rcap);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const unsigned egrid = (unsigned)((a.count + 3) / 4);
+    hipLaunchKernelGGL(k1_emit, dim3(egrid), dim3(256), 0, st, a, (const uint4 *)recs, rcap);
+    return hipGetLastError();
+}
+
+// The property T16 relies on, checked once per process on the device:
+// same-address ds_write_b16 of one wave instruction land in ascending lane
+// order (the highest lane's value stays).
+__global__ void k_lds_store_order(uint32_t *res) {
+    __shared__ uint16_t t[8];
+    const uint32_t l = threadIdx.x;
+    if (l < 8) t[l] = 0;
+    __syncthreads();
+    t[l & 7] = (uint16_t)(l + 1);
+    __syncthreads();
+    if (l < 8 && t[l] != (uint16_t)(56 + l + 1)) atomicAdd(res, 1u);
+}
+
+}  // namespace
+
+bool lds_exchange_in_lane_order();
+
+bool lds_store_in_lane_order() {
+    static int ok = -1;
+    if (ok >= 0) return ok == 1;
+    ok = 0;
+    uint32_t *d = nullptr, h = 1;
+    hipStream_t st = nullptr;
+    if (hipMalloc(&d, sizeof(uint32_t)) != hipSuccess) return false;
+    if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
+        if (hipMemsetAsync(d, 0, sizeof(uint32_t), st) == hipSuccess) {
+            hipLaunchKernelGGL(k_lds_store_order, dim3(1), dim3(64), 0, st, d);
+            if (hipGetLastError() == hipSuccess && hipMemcpyAsync(&h, d, sizeof(uint32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
+                hipStreamSynchronize(st) == hipSuccess)
+                ok = h == 0 ? 1 : 0;
+        }
+        (void)hipStreamDestroy(st);
+    }
+    (void)hipFree(d);
+    return ok == 1;
+}
+
+// the table the batch takes: 16 (T16), 32 (T32) or 0 (K1s cannot take it)
+static int split_table(const CompressArgs &a) {
+    if (a.count > (1ull << 31)) return 0;
+    const int G = split_g();
+    if (!split_t32_forced() && (G == 8 ? split_stride<8, true>(a) : split_stride<16, true>(a)) != 0 && lds_store_in_lane_order())
+        return 16;
+    if ((G == 8 ? split_stride<8, false>(a) : split_stride<16, false>(a)) != 0 && lds_exchange_in_lane_order()) return 32;
+    return 0;
+}
+
+void select_split_table(bool t32) { g_split_t32 = t32; }
+
+uint32_t split_stride_words(const CompressArgs &a) { return split_table(a) != 0 ? 1u : 0u; }
+
+uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a.max_len) * 4; }
+
+hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t st) {
+    uint4 *recs = (uint4 *)scratch;
+    const int G = split_g(), T = split_table(a);
+    if (T == 16) return G == 8 ? launch_split_g<8, true>(a, recs, st) : launch_split_g<16, true>(a, recs, st);
+    return G == 8 ? launch_split_g<8, false>(a, recs, st) : launch_split_g<16, false>(a, recs, st);
+}
+
+}  // namespace ez

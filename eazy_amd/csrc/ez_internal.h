@@ -80,8 +80,15 @@ hipError_t launch_compress_lane(const CompressArgs &a, uint16_t *scratch, hipStr
 uint32_t tile_stride_words(const CompressArgs &a);
 bool lds_exchange_in_lane_order();  // the hardware property K1t relies on (checked once)
 hipError_t launch_compress_tile(const CompressArgs &a, hipStream_t s);
+// K1s: fresh streams, parse kernel + token-writer kernel (ez_compress_split.hip);
+// scratch = 16-byte match records, split_scratch_words u32 words
+uint32_t split_stride_words(const CompressArgs &a);
+uint64_t split_scratch_words(const CompressArgs &a);
+void select_split_table(bool t32);  // force the u32 exchange table (tests, A/B)
+hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t s);
 // the K1 variant a batch launch takes: 'l' lane, 'g' g16, 'f' fresh wave, 'w' general wave
 char compress_variant(const CompressArgs &a);
+void select_compress_variant(int v);  // 0 = automatic, else a variant letter (tests, A/B)
 // K1g: fresh streams, 16 lanes per stream (ez_compress_g16.hip)
 uint32_t g16_stride_words(const CompressArgs &a);
 hipError_t launch_compress_g16(const CompressArgs &a, hipStream_t s);

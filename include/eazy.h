@@ -159,9 +159,15 @@ int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *works
 
 /* Introspection (no reference counterpart): the K1 kernel a batch of `count`
  * fresh streams of <= max_len bytes would run on the current device, as a
- * character: 't' tile (exchange visits), 'r' grp, 'l' lane, 'g' g16,
+ * character: 's' split (parse + token writer), 't' tile (exchange visits), 'r' grp, 'l' lane, 'g' g16,
  * 'f' fresh wave, 'w' general wave; EZ_EDEVICE (negated) without a device. */
 int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t count);
+/* Testing / A-B measurement (no reference counterpart): force the K1 kernel of
+ * later batch calls in this process ('s' split, 'S' split with the u32
+ * exchange table, 't' tile, 'r', 'l', 'g', 'f',
+ * 'w'; 0 = automatic choice).  A forced kernel that cannot take a batch falls
+ * back to the automatic choice.  Not thread-safe against concurrent calls. */
+int ez_select_compress_kernel(int kind);
 
 #ifdef __cplusplus
 }

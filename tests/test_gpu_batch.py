@@ -13,6 +13,17 @@ pytestmark = pytest.mark.gpu
 MiB = 1 << 20
 
 
+@pytest.fixture(params=["", "S", "t"], ids=["auto", "split32", "tile"], autouse=True)
+def k1_kind(request):
+    """Every batch test runs on the automatic K1 choice (K1s with the u16
+    table at these shapes), K1s with the u32 exchange table, and K1t."""
+    import eazy_amd as ez
+
+    ez.select_compress_kernel(request.param)
+    yield request.param
+    ez.select_compress_kernel("")
+
+
 def _run(cuda, bufs, block=MiB, htable=1024, magic=True):
     import torch
 
@@ -133,12 +144,14 @@ def test_larger_than_window(cuda):
     _check(cuda, bufs, 1024, 32)
 
 
-def test_tile_kernel_selected(cuda):
-    """The C1 shape runs K1t, whose visits rely on same-address LDS exchanges
-    applying in ascending lane order: the library checks that on the device
-    (tools/mb_ldsatomic.hip shows the measurement) and would fall back to
-    K1grp if it failed, so 't' here means the property holds on this GPU."""
+def test_split_kernel_selected(cuda, k1_kind):
+    """The C1 shape runs K1s (parse + token writer) unless a test forces
+    another kernel; K1s and K1t rely on same-address LDS stores / exchanges of
+    one wave instruction applying in ascending lane order, which the library
+    checks on the device (tools/mb_ldsatomic.hip shows the measurement) before
+    choosing them."""
     import eazy_amd as ez
 
-    assert ez.compress_kernel(MiB, 1024, 4096, 65536) == "t"
-    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) != "t"  # 2n > block: the general kernel
+    want = {"": "s", "S": "s", "t": "t"}[k1_kind]
+    assert ez.compress_kernel(MiB, 1024, 4096, 65536) == want
+    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) not in "st"  # 2n > block: the general kernel
