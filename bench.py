@@ -30,7 +30,30 @@ WORKLOADS = {
     # name: (streams per GPU, bytes per stream, block, htable, description)
     "c1": (65536, 4096, 1 << 20, 1024, "c1: 65536 x 4 KiB log-like streams per GPU, block 1 MiB, htable 1024"),
     "c2": (4096, 256 << 10, 1 << 20, 1024, "c2: 4096 x 256 KiB log-like streams per GPU, block 1 MiB, htable 1024"),
+    # C4, the gradient-wire retarget: tensor buckets bit-cast to bytes (Writes longer than the window)
+    "c4": (64, 4 << 20, 1 << 20, 1024, "c4: 64 x 4 MiB fp32 N(0,1e-3) gradient buckets per GPU, block 1 MiB, htable 1024"),
+    "c4h": (64, 4 << 20, 1 << 20, 1024, "c4h: 64 x 4 MiB bf16 N(0,1e-3) gradient buckets per GPU, block 1 MiB, htable 1024"),
+    "c4s": (64, 4 << 20, 1 << 20, 1024, "c4s: 64 x 4 MiB fp32 buckets, 90% zeros, block 1 MiB, htable 1024"),
 }
+
+
+def workload_bytes(name, seed, total):
+    """Host bytes of a workload (seeded): log events, or gradient buckets."""
+    import numpy as np
+
+    from eazy_amd import synth
+
+    if name in ("c1", "c2"):
+        return synth.logs(seed, total), "synthetic (seeded tlwire-like log events, eazy_amd/tools/synth.c)"
+    if name == "c4h":
+        f = synth.f32(seed, total // 2)
+        return (f.view(np.uint32) >> 16).astype(np.uint16).view(np.uint8), "synthetic (seeded bf16 = top half of N(0,1e-3) fp32)"
+    f = synth.f32(seed, total // 4)
+    if name == "c4s":
+        rng = np.random.default_rng(seed)
+        f[rng.random(f.shape[0]) < 0.9] = 0.0
+        return f.view(np.uint8), "synthetic (seeded N(0,1e-3) fp32, 90% zeros)"
+    return f.view(np.uint8), "synthetic (seeded N(0,1e-3) fp32)"
 
 
 def parse():
@@ -162,7 +185,7 @@ def main():
         count = args.streams
         desc += f" (stream count overridden: {count})"
     total = count * size
-    host = synth.logs(ezd.seed(1000, R), total)  # this rank's shard of independent streams
+    host, data_desc = workload_bytes(args.workload, ezd.seed(1000, R), total)  # this rank's shard of independent streams
     offs = synth.batch_offsets(count, size)
     if args.same:
         host = np.tile(host[:size], count)
@@ -251,7 +274,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (seeded tlwire-like log events, eazy_amd/tools/synth.c)",
+        "data": data_desc,
         "config": {
             "workload": desc,
             "streams_per_gpu": count,

@@ -145,6 +145,12 @@ def select_compress_kernel(kind: str = "") -> None:
     _check(_lib().ez_select_compress_kernel(ord(kind) if kind else 0))
 
 
+def select_decompress_kernel(kind: str = "") -> None:
+    """Force the first K2 kernel of later batch decodes ('f', 'g'; '' =
+    automatic).  Tests and A/B measurement only."""
+    _check(_lib().ez_select_decompress_kernel(ord(kind) if kind else 0))
+
+
 def _check(code: int, detail: int = 0) -> None:
     if code == OK:
         return

@@ -525,6 +525,12 @@ extern "C" int ez_select_compress_kernel(int kind) {
     return EZ_OK;
 }
 
+extern "C" int ez_select_decompress_kernel(int kind) {
+    if (kind != 0 && kind != 'f' && kind != 'g') return EZ_EINVAL;
+    ez::select_decompress_variant(kind);
+    return EZ_OK;
+}
+
 extern "C" size_t ez_decompress_workspace(uint64_t count) {
     return (size_t)ez::decompress_workspace_words(count) * sizeof(uint32_t);
 }

@@ -36,9 +36,9 @@
 //       inserts of lanes Go does not visit are undone with one ds_min_u32,
 //       which needs inserts monotone in position: windows that start at or
 //       below the highest inserted position are judged one position at a time.
-// Acceptance is decided with 8-byte capped counts (minCopyChunk = 6 < 8,
-// writer.go:119, 301); only a saturated count is extended, forward and
-// backward at once, 16 bytes per lane.  Each accepted match advances `done` by
+// Acceptance is decided with capped counts, 24 bytes forward and 8 backward
+// (minCopyChunk = 6 < 8, writer.go:119, 301); only a saturated count is
+// extended, forward and backward at once, 16 bytes per lane.  Each accepted match advances `done` by
 // its copy length (>= 6), so a stream of n bytes makes at most n/6 records.
 #include "ez_format.h"
 #include "ez_internal.h"
@@ -90,21 +90,22 @@ __device__ __forceinline__ V16 src16(const GW &P, int32_t y, int mode, int32_t d
     return mode == 2 ? keep_low16(v, done - y) : v;
 }
 
-// Exact forward and backward match counts of one group at once, past the 8
-// bytes the capped judgement already compared: lanes 0..G/2-1 scan forward
+// Exact forward and backward match counts of one group at once, past the
+// bytes the capped judgement already compared (fromf forward, 8 backward):
+// lanes 0..G/2-1 scan forward
 // (a+k vs b+k), lanes G/2..G-1 backward (a-1-k vs b-1-k), 16 bytes per lane
-// per step, so a count below 8 + 8G bytes costs one load round trip.
+// per step, so a count below fromf + 8G bytes costs one load round trip.
 template <int G>
 __device__ __forceinline__ void gext(const GW &P, bool runf, bool runb, int g, int lj, int32_t a, int32_t b, int mode,
-                                     int32_t done, int32_t limf, int32_t limb, int32_t &resf, int32_t &resb) {
+                                     int32_t done, int32_t fromf, int32_t limf, int32_t limb, int32_t &resf, int32_t &resb) {
     constexpr int H = G / 2;
     constexpr uint32_t kHalf = (1u << H) - 1;
     const bool fw = lj < H;
     const int t = lj % H;
-    resf = 8 < limf ? 8 : limf;
+    resf = fromf < limf ? fromf : limf;
     resb = 8 < limb ? 8 : limb;
-    bool gof = runf && 8 < limf, gob = runb && 8 < limb;
-    int32_t basef = 8, baseb = 8;
+    bool gof = runf && fromf < limf, gob = runb && 8 < limb;
+    int32_t basef = fromf, baseb = 8;
     while (__ballot(gof || gob) != 0) {
         const bool mine = fw ? gof : gob;
         const int32_t lim = fw ? limf : limb;
@@ -204,8 +205,12 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
     int32_t i = 0, done = 0, hiw = -1, nrec = 0;  // hiw: highest position in the table (T32)
     bool live = have && n >= 4 && !err;
     int32_t guard = 4 * n + 64;
-    uint64_t pxb = 0, pxf = 0;  // bytes before / from this lane's position (loaded one window ahead)
-    if (live) P.around(i + lj, pxb, pxf);
+    // bytes x-8 .. x+23 around this lane's position x (loaded one window ahead)
+    uint64_t pxb = 0, pxf = 0, px2 = 0, px3 = 0;
+    if (live) {
+        P.around(i + lj, pxb, pxf);
+        P.around(i + lj + 16, px2, px3);
+    }
 #if (EZ_EXP & 4)
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime(), prof_it = 0;
 #endif
@@ -233,9 +238,12 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
 
         // ---- capped judgement (exact decision), writer.go:219-301, writeRunlen :441-463
         bool acc = false;
-        int32_t info = 0;  // cand | forward count << 20 | backward count << 24 | rl << 28 | zr << 29
-        uint64_t pcb = 0, pcf = 0;
-        if (valid) P.around(cand, pcb, pcf);
+        int32_t info = 0;  // cand | forward count << 20 | backward count << 25 | rl << 29 | zr << 30
+        uint64_t pcb = 0, pcf = 0, pc2 = 0, pc3 = 0;
+        if (valid) {
+            P.around(cand, pcb, pcf);
+            P.around(cand + 16, pc2, pc3);
+        }
         EZ_PROF_MARK(5);
         if (valid) {
             const bool rl = cand >= done && cand < x;
@@ -243,13 +251,21 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
             const int32_t bl = rl ? ((x - done) < cand ? (x - done) : cand) : x - done;
             int32_t jb = clz_bytes(pxb ^ pcb);
             jb = jb < bl ? jb : bl;
-            int32_t jf = ctz_bytes(pxf ^ (rl ? pcf : low_bytes(pcf, done - cand)));
+            // forward, 24 bytes capped; the window branch compares the ring image (0 from done on)
+            V16 c2{pc2, pc3};
+            if (!rl) c2 = keep_low16(c2, done - cand - 8);
+            const uint64_t d0 = pxf ^ (rl ? pcf : low_bytes(pcf, done - cand));
+            const uint64_t d1 = px2 ^ c2.lo, d2 = px3 ^ c2.hi;
+            int32_t jf = d0 ? ctz_bytes(d0) : (d1 ? 8 + ctz_bytes(d1) : 16 + ctz_bytes(d2));
             jf = jf < n - x ? jf : n - x;
             acc = rl ? (zr || jf + jb >= kMinCopyChunk) : ((jf < done - cand ? jf : done - cand) + jb >= kMinCopyChunk);
             int32_t zb = clz_bytes(pcb);
             zb = zb < cand - done ? zb : cand - done;
-            const int32_t fk = zr ? 8 : jf, bk = zr ? zb : jb;
-            info = cand | (fk << 20) | (bk << 24) | ((int32_t)rl << 28) | ((int32_t)zr << 29);
+            // zero region: the zeros from cand on, 24 bytes capped
+            int32_t zf = pc2 ? 8 + ctz_bytes(pc2) : 16 + ctz_bytes(pc3);
+            zf = zf < n - cand ? zf : n - cand;
+            const int32_t fk = zr ? zf : jf, bk = zr ? zb : jb;
+            info = cand | (fk << 20) | (bk << 25) | ((int32_t)rl << 29) | ((int32_t)zr << 30);
         }
         EZ_PROF_MARK(1);
         const uint32_t am = gball<G>(acc, g);
@@ -266,15 +282,15 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
         const uint32_t h1v = (uint32_t)bcast((int32_t)h, G * g + (a + 1 < G ? a + 1 : G - 1));
         const bool act = live && a >= 0;
         const int32_t xa = i + a;
-        const int32_t ca = ib & 0xfffff, fk = (ib >> 20) & 0xf, bk8 = (ib >> 24) & 0xf;
-        const bool rl = (ib >> 28) & 1, zr = (ib >> 29) & 1;
+        const int32_t ca = ib & 0xfffff, fk = (ib >> 20) & 0x1f, bk8 = (ib >> 25) & 0xf;
+        const bool rl = (ib >> 29) & 1, zr = (ib >> 30) & 1;
         const int mode = zr ? 0 : (rl ? 1 : 2);
         const int32_t fa = zr ? ca : xa;
         EZ_PROF_MARK(2);
         const int32_t blim = zr ? ca - done : (rl ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
         int32_t fx, cx;
-        gext<G>(P, act && fk == 8, act && bk8 == 8, g, lj, fa, ca, mode, done, n - fa, blim, fx, cx);
-        const int32_t f = fk == 8 ? fx : fk;
+        gext<G>(P, act && fk == 24, act && bk8 == 8, g, lj, fa, ca, mode, done, 24, n - fa, blim, fx, cx);
+        const int32_t f = fk == 24 ? fx : fk;
         const int32_t c = bk8 == 8 ? cx : bk8;
         EZ_PROF_MARK(3);
         int32_t lit_end = 0, nxt = 0;
@@ -301,7 +317,10 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
         if (live && (err || i + 4 > n)) live = false;
         // the next window's bytes, in flight while this window's table writes and record go out
         EZ_PROF_MARK(6);
-        if (live) P.around(i + lj, pxb, pxf);
+        if (live) {
+            P.around(i + lj, pxb, pxf);
+            P.around(i + lj + 16, px2, px3);
+        }
         EZ_PROF_MARK(7);
 
         // ---- T16: the lanes Go visits store their positions (the last of a hash wins)

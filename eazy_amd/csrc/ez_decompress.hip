@@ -326,9 +326,13 @@ __device__ __forceinline__ void fast_one(const DecompressArgs &A, const uint64_t
 }
 
 // grid-stride over streams (EZ_K2_WAVES caps the streams in flight, experiments)
-__global__ __launch_bounds__(256) void k2_fast(DecompressArgs A) {
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < A.count; s += (uint64_t)gridDim.x * blockDim.x)
-        fast_one(A, s);
+// spw: streams per wave (64 = every lane; fewer = more waves per SIMD to hide latency)
+__global__ __launch_bounds__(256) void k2_fast(DecompressArgs A, uint32_t spw) {
+    const uint64_t todo = A.todo ? (uint64_t)A.todo[0] : A.count;
+    const uint32_t l = threadIdx.x & 63;
+    if (l >= spw) return;
+    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t k = w * spw + l; k < todo; k += nw * spw) fast_one(A, A.todo ? (uint64_t)A.todo[1 + k] : k);
 }
 
 __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
@@ -388,7 +392,11 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
 
 }  // namespace
 
-uint64_t decompress_workspace_words(uint64_t count) { return count + 16; }
+// two stream lists: K2g -> k2_fast hand-overs, k2_fast -> exact decoder hand-overs
+static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'f', 'g'
+void select_decompress_variant(int v) { g_decompress_variant = v; }
+
+uint64_t decompress_workspace_words(uint64_t count) { return 2 * count + 32; }
 
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;
@@ -397,8 +405,10 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
         return hipGetLastError();
     }
+    // long streams (slots of 64 KiB and more, C2/C4): a lane per stream moves 16 bytes per
+    // dependent step and few streams fill few lanes; the wave-per-stream decoder moves 64
     static const bool use_exact = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "exact") == 0;
-    if (use_exact) {
+    if (use_exact || a.max_out >= (64u << 10)) {
         DecompressArgs b = a;
         b.slow = nullptr;
         uint64_t grid = b.count < (1u << 30) ? b.count : (1u << 30);
@@ -407,21 +417,35 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     }
     hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
-    // EZ_K2=grp: the LDS-resident group decoder (ez_decompress_grp.hip) for small streams
-    static const bool use_grp = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "grp") == 0;
-    const uint32_t R = use_grp ? grp_decode_region(a.max_out) : 0;
-    if (R) {
-        e = launch_decompress_grp(a, R, st);
+    // K2g (LDS group decoder) first when the slots are small; its hand-overs go
+    // through k2_fast, whose hand-overs go to the exact decoder
+    // K2g is opt-in: at C1 the lane-per-stream decoder is faster
+    if (g_decompress_variant < 0) g_decompress_variant = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "group") == 0 ? 'g' : 0;
+    const uint32_t RG = g_decompress_variant == 'g' ? group_decode_region(a.max_out) : 0;
+    if (RG) {
+        uint32_t *list2 = a.slow + a.count + 16;
+        e = hipMemsetAsync(list2, 0, sizeof(uint32_t), st);
         if (e != hipSuccess) return e;
-        uint64_t grid = a.count < 4096 ? a.count : 4096;
-        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+        e = launch_decompress_group(a, RG, st);
+        if (e != hipSuccess) return e;
+        DecompressArgs f = a;
+        f.todo = a.slow;
+        f.slow = list2;
+        const uint64_t fgrid = (a.count + 255) / 256;
+        hipLaunchKernelGGL(k2_fast, dim3((unsigned)fgrid), dim3(256), 0, st, f, 64u);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        const uint64_t grid = a.count < 4096 ? a.count : 4096;
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, f);
         return hipGetLastError();
     }
     static const unsigned blk = getenv("EZ_K2_BLOCK") ? (unsigned)atoi(getenv("EZ_K2_BLOCK")) : 256u;
     static const uint64_t maxw = getenv("EZ_K2_WAVES") ? (uint64_t)atoll(getenv("EZ_K2_WAVES")) : 0;
-    uint64_t fgrid = (a.count + blk - 1) / blk;
+    static const uint32_t spw = getenv("EZ_K2_SPW") ? (uint32_t)atoi(getenv("EZ_K2_SPW")) : 64u;
+    const uint64_t lanes = (a.count + spw - 1) / spw * 64;  // threads launched
+    uint64_t fgrid = (lanes + blk - 1) / blk;
     if (maxw && fgrid * blk / 64 > maxw) fgrid = (maxw * 64 + blk - 1) / blk;
-    hipLaunchKernelGGL(k2_fast, dim3((unsigned)fgrid), dim3(blk), 0, st, a);
+    hipLaunchKernelGGL(k2_fast, dim3((unsigned)fgrid), dim3(blk), 0, st, a, spw);
     // exact decoder over the handed-over streams (count read on the device)
     uint64_t grid = a.count < 4096 ? a.count : 4096;
     hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);

@@ -62,6 +62,7 @@ struct DecompressArgs {
     DecodeState *st;          // handle: state in/out
     uint32_t *slow;           // batch: [0] = count, [1..] = streams the fast path handed over (nullptr = exact path only)
     uint64_t max_out;         // batch: host hint, largest output slot (0 = unknown)
+    const uint32_t *todo;     // batch, k2_fast: [0] = count, [1..] = the streams to decode (nullptr = all)
 };
 
 // words of workspace the two-level batch decoder needs
@@ -95,9 +96,10 @@ hipError_t launch_compress_g16(const CompressArgs &a, hipStream_t s);
 // u32 words of global hash-table scratch a batch launch needs (hs too big for LDS)
 uint64_t compress_scratch_words(const CompressArgs &a);
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t s);
-// K2grp: LDS region per stream for streams of <= max_out output bytes (0 = not usable)
-uint32_t grp_decode_region(uint64_t max_out);
-hipError_t launch_decompress_grp(const DecompressArgs &a, uint32_t R, hipStream_t s);
+// K2g: G lanes per stream, compressed bytes and history in LDS (ez_decompress_group.hip)
+uint32_t group_decode_region(uint64_t max_out);
+hipError_t launch_decompress_group(const DecompressArgs &a, uint32_t R, hipStream_t s);
+void select_decompress_variant(int v);  // 0 = automatic, 'f' fast, 'g' group (tests, A/B)
 hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
                        uint8_t *packed, uint64_t *packed_off, void *workspace, hipStream_t s);
 size_t pack_workspace(uint64_t count);

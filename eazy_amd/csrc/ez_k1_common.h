@@ -50,8 +50,13 @@ struct GW {
     __device__ __forceinline__ void around(int32_t y, uint64_t &before, uint64_t &from) const {
         const uint8_t *a = p + y - 8;
         V16 v;
-        if (y >= 8 && a + 16 <= bhi) {
+        if (a >= blo && a + 16 <= bhi) {
             v = ld16v(a);  // the common case: one unaligned 16-byte load
+            if (y < 8) {   // near the stream start: the bytes before it read 0
+                const int32_t k = 8 - y;
+                v.lo &= k >= 8 ? 0ull : ~0ull << (8 * k);
+                v.hi &= k >= 16 ? 0ull : (k <= 8 ? ~0ull : ~0ull << (8 * (k - 8)));
+            }
         } else {
             v = V16{0, 0};
             if (bhi - blo >= 16) {

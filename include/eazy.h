@@ -168,6 +168,10 @@ int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t
  * 'w'; 0 = automatic choice).  A forced kernel that cannot take a batch falls
  * back to the automatic choice.  Not thread-safe against concurrent calls. */
 int ez_select_compress_kernel(int kind);
+/* Testing / A-B measurement: the first K2 kernel of later batch decodes with a
+ * workspace and a max_len hint ('f' lane-per-stream, 'g' LDS group decoder;
+ * 0 = automatic).  Streams either cannot take go on to the exact decoder. */
+int ez_select_decompress_kernel(int kind);
 
 #ifdef __cplusplus
 }

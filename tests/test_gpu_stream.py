@@ -166,9 +166,13 @@ def test_batch_decoders_on_damaged_streams(cuda):
     coff = torch.from_numpy(offs).to(cuda)
     for cap in (4096, 8192):
         ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-        for kw in ({"max_len": cap}, {}, {"exact_only": True}):
-            out, sizes, status = ez.decompress_batch(comp, coff, ooff, **kw)
-            torch.cuda.synchronize()
+        for kind, kw in (("", {"max_len": cap}), ("g", {"max_len": cap}), ("", {}), ("", {"exact_only": True})):
+            ez.select_decompress_kernel(kind)
+            try:
+                out, sizes, status = ez.decompress_batch(comp, coff, ooff, **kw)
+                torch.cuda.synchronize()
+            finally:
+                ez.select_decompress_kernel("")
             _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
 
 
