@@ -517,7 +517,9 @@ hipError_t launch_split_g(const CompressArgs &a, uint4 *recs, hipStream_t st) {
     const uint32_t stride = split_stride<G, T16>(a);
     const uint64_t rcap = rec_cap(a.max_len);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
-    hipLaunchKernelGGL((k1_parse<G, T16>), dim3(grid), dim3(64), (size_t)stride * 4 * S, st, a, stride, recs, rcap);
+    // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
+    static const size_t pad = getenv("EZ_K1S_LDSPAD") ? (size_t)atoi(getenv("EZ_K1S_LDSPAD")) : 0;
+    hipLaunchKernelGGL((k1_parse<G, T16>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, recs, rcap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
