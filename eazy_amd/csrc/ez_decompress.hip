@@ -420,7 +420,10 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     // K2g (LDS group decoder) first when the slots are small; its hand-overs go
     // through k2_fast, whose hand-overs go to the exact decoder
     // K2g is opt-in: at C1 the lane-per-stream decoder is faster
-    if (g_decompress_variant < 0) g_decompress_variant = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "group") == 0 ? 'g' : 0;
+    if (g_decompress_variant < 0) {
+        const char *v = getenv("EZ_K2");
+        g_decompress_variant = v && strcmp(v, "group") == 0 ? 'g' : (v && strcmp(v, "fast") == 0 ? 'f' : 0);
+    }
     const uint32_t RG = g_decompress_variant == 'g' ? group_decode_region(a.max_out) : 0;
     if (RG) {
         uint32_t *list2 = a.slow + a.count + 16;
@@ -437,6 +440,14 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         if (e != hipSuccess) return e;
         const uint64_t grid = a.count < 4096 ? a.count : 4096;
         hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, f);
+        return hipGetLastError();
+    }
+    if (g_decompress_variant != 'f') {
+        // K2r (default): k2_fast with the recent output in an LDS ring
+        e = launch_decompress_ring(a, st);
+        if (e != hipSuccess) return e;
+        const uint64_t grid = a.count < 4096 ? a.count : 4096;
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
         return hipGetLastError();
     }
     static const unsigned blk = getenv("EZ_K2_BLOCK") ? (unsigned)atoi(getenv("EZ_K2_BLOCK")) : 256u;

@@ -1,0 +1,206 @@
+// ez_decompress_ring.hip — K2r: batch decompression, one lane per stream, the
+// last 512 decoded bytes of every stream in an LDS ring.
+//
+// Restates Reader.Read to EOF for NewReaderBytes (reader.go:116-216 read,
+// readTag :218-270, continueMetaTag :272-325, reset :327-344, Decoder
+// :346-514) for the common case, exactly as k2_fast (ez_decompress.hip) does —
+// header metas, padding, breaks, literal and copy tokens; anything else hands
+// the stream to the exact decoder — and differs in where a copy reads from.
+//
+// Why.  k2_fast reads every back-reference from the output it wrote to HBM a
+// few tokens earlier; 64 lanes of a wave touch 64 unrelated streams, and at
+// C1 the 8,192 streams in flight per XCD keep ~5 MB of recently written lines
+// live against a 4 MB L2 (PMC: 43 % L2 misses).  Most distances are short
+// (median 365 bytes on the C1 logs), so each lane keeps its stream's last 512
+// output bytes in LDS (ring[p & 511] = output byte p, plus a 16-byte mirror of
+// the ring's first bytes after its end so that any 16-byte read is one
+// contiguous LDS access): copies with distance <= 496 read the ring, farther
+// ones read HBM as before.  The ring starts zeroed, which is the fresh
+// window's zero history: a position before the stream start
+// maps to a ring slot that has not been written yet.  The output reaches HBM
+// from the ring in whole 128-byte lines once they are final, instead of one
+// 16-byte partial-line store per move (the stores cost half of k2_fast's time:
+// 1.37 -> 0.69 ms with them removed).  One block of 256 lanes per CU (4
+// waves, one per SIMD) holds 256 rings of 528 bytes.
+#include "ez_format.h"
+#include "ez_internal.h"
+#include "ez_wave.h"
+#include "ez_bytes.h"
+
+namespace ez {
+namespace {
+
+constexpr int32_t kRing = 512;           // ring bytes per stream (power of two)
+constexpr int32_t kRingStride = kRing + 16;  // + the mirror of bytes 0..15
+constexpr int32_t kNear = kRing - 16;    // copies this close read the ring
+constexpr int kRingBlock = 256;          // lanes per block (one wave per SIMD of a CU)
+constexpr int32_t kChunk = 128;          // output leaves the ring in whole 128-byte lines
+
+typedef uint64_t __attribute__((aligned(1))) u64_ua;
+
+__device__ __forceinline__ V16 ring_ld(const uint8_t *ring, int32_t p) {
+    const uint8_t *q = ring + (p & (kRing - 1));
+    return V16{*(const u64_ua *)q, *(const u64_ua *)(q + 8)};
+}
+// 16 bytes of output position p into the ring, keeping the mirror equal to bytes 0..15
+__device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v) {
+    const int32_t r = p & (kRing - 1);
+    *(u64_ua *)(ring + r) = v.lo;
+    *(u64_ua *)(ring + r + 8) = v.hi;
+    if (r + 16 > kRing) put_small(ring, shr16(v, (uint32_t)(kRing - r)), (uint32_t)(r + 16 - kRing));
+    if (r == 0) {
+        *(u64_ua *)(ring + kRing) = v.lo;
+        *(u64_ua *)(ring + kRing + 8) = v.hi;
+    } else if (r < 16) {
+        put_small(ring + kRing + r, v, (uint32_t)(16 - r));  // (put_small takes < 16 bytes)
+    }
+}
+
+__device__ __forceinline__ void ring_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring) {
+    const uint8_t *b = A.in + A.in_off[s];
+    const int64_t nb64 = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
+    const uint8_t *in_end = A.in + A.in_off[A.count];  // loads never pass the last stream's end
+    uint8_t *out = A.out + A.out_off[s];
+    const int64_t cap64 = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    const int64_t limit = A.block_size_limit;
+    // 32-bit positions; clamped loads need >= 16 input bytes in the batch and a 16-byte slot
+    bool slow = in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16;
+    const int32_t nb = slow ? 0 : (int32_t)nb64, cap = (int32_t)cap64;
+    for (int32_t k = 0; k < kRingStride; k += 16) {
+        *(u64_ua *)(ring + k) = 0;
+        *(u64_ua *)(ring + k + 8) = 0;
+    }
+    int32_t i = 0, pos = 0, bsl = -1;  // bsl: log2 of the window after MetaReset (-1: none yet)
+    V16 h{0, 0};                       // 16 bytes at b + i (the next header)
+    if (!slow) h = b + 16 <= in_end ? ld16v(b) : ld_clamped(b, A.in, in_end);
+    // the token being written: rem bytes at dst from sp (input / HBM output) or from the ring
+    int32_t rem = 0, dst = 0, step = 16, rp = 0, fl = 0;  // fl: output below it is in HBM
+    const uint8_t *sp = b;
+    bool from_in = false, patt = false, near = false;
+    V16 pv{0, 0};
+    for (;;) {
+        if (rem == 0) {
+            if (i >= nb) break;
+            const uint64_t lo = h.lo;
+            const uint32_t t0 = (uint32_t)lo & 0xff, l7 = t0 & 0x7f;
+            int32_t adv;
+            if (t0 == 0 || t0 == 0x80) {
+                if (t0 == 0) {  // padding (reader.go:221-224), a run of zero bytes at once
+                    adv = lo ? (int32_t)(__builtin_ctzll(lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
+                } else {
+                    // meta (continueMetaTag reader.go:272-325): header metas and breaks only
+                    const uint32_t mb = (uint32_t)(lo >> 8) & 0xff, mt = mb & 0xf8, ml = mb & 7;
+                    const int32_t mln = ml == 7 ? 0 : (1 << ml);
+                    const uint32_t marg = (uint32_t)(lo >> 16) & 0xff;
+                    const bool m_brk = mt == kMetaBreak && mln == 0;
+                    const bool m_rst = mt == kMetaReset && mln == 1 && marg <= 32 && pos == 0 && (limit == 0 || (1ll << marg) <= limit);
+                    const bool m_ver = mt == kMetaVer && mln == 1 && marg == 0;
+                    const bool m_mag = mt == kMetaMagic && mln == 4 && (uint32_t)(lo >> 16) == 0x797a6165u;
+                    if (ml == 6 || i + 2 + mln > nb || !(m_brk || m_rst || m_ver || m_mag)) { slow = true; break; }
+                    if (m_rst) bsl = (int32_t)marg;
+                    adv = 2 + mln;
+                }
+            } else {
+                // Decoder.Tag reader.go:346-392 and Decoder.Offset :394-420, by selects
+                const uint32_t lx = (uint32_t)(lo >> 8);
+                const int64_t L = l7 < 124 ? (int64_t)l7
+                                : (l7 == 124 ? 124 + (int64_t)(lx & 0xff) : (l7 == 125 ? 380 + (int64_t)(lx & 0xffff) : 65916 + (int64_t)lx));
+                const uint32_t j = l7 < 124 ? 1 : (l7 == 124 ? 2 : (l7 == 125 ? 3 : 5));
+                const bool cp = (t0 & 0x80) != 0;
+                const uint64_t x = fun8(lo, h.hi, j);  // bytes from the offset on (header <= 11 bytes)
+                const bool lng = (x & 0xff) == 0xff;
+                const uint64_t y = lng ? fun8(lo, h.hi, j + 1) : x;
+                const uint32_t o = (uint32_t)y & 0xff, ox = (uint32_t)(y >> 8);
+                const int64_t D0 = o < 252 ? (int64_t)o : (o == 252 ? 252 + (int64_t)(ox & 0xff) : (o == 253 ? 508 + (int64_t)(ox & 0xffff) : 66044 + (int64_t)ox));
+                const uint32_t k = o < 252 ? 1 : (o == 252 ? 2 : (o == 253 ? 3 : 5));
+                const int64_t D = lng ? D0 : D0 + L;
+                adv = cp ? (int32_t)(j + (lng ? 1 : 0) + k) : (int32_t)(j + L);
+                const int64_t bs = bsl < 0 ? 0 : (1ll << bsl);
+                const bool bad = l7 == 127 || (cp && o == 255) || (limit != 0 && L > limit) || bs == 0 ||
+                                 pos + L > cap || (int64_t)i + (cp ? (int64_t)adv : (int64_t)j + L) > nb || (cp && D > bs);
+                if (bad) { slow = true; break; }  // the exact decoder takes the stream
+                dst = pos;
+                rem = (int32_t)L;
+                pos += (int32_t)L;
+                from_in = !cp;
+                near = cp && D <= kNear;
+                rp = dst - (int32_t)D;
+                sp = cp ? out + rp : b + (i + (int32_t)j);
+                patt = cp && D < 16;
+                step = 16;
+                if (!cp && (int64_t)j + L <= 16) {  // a short literal is in the header's 16 bytes already
+                    patt = true;
+                    pv = shr16(h, j);
+                }
+                if (patt && cp) {
+                    // zero region (D == 0, reader.go:176-179) or a short-period run:
+                    // one 16-byte pattern stored every `step` bytes
+                    if (D == 0) {
+                        pv = V16{0, 0};
+                    } else {
+                        const uint32_t per = (uint32_t)D;
+                        pv = run_pattern(shr16(ring_ld(ring, dst - 16), 16 - per), per);
+                        step = (int32_t)(per * (16 / per));
+                    }
+                }
+            }
+            i += adv;
+            // the next header, loaded beside this token's first move
+            if (i < nb) h = b + i + 16 <= in_end ? ld16v(b + i) : ld_clamped(b + i, A.in, in_end);
+        }
+        if (rem > 0) {
+            V16 v;
+            if (patt) v = pv;
+            else if (near) v = ring_ld(ring, rp);
+            else if (from_in ? sp + 16 > in_end : sp < out) v = from_in ? ld_clamped(sp, A.in, in_end) : ld_clamped(sp, out, out + cap);
+            else v = ld16v(sp);
+            ring_st(ring, dst, v);
+            const int32_t kk = rem < step ? rem : step;
+            dst += kk;
+            sp += kk;
+            rp += kk;
+            rem -= kk;
+            // a finished 128-byte chunk of output leaves the ring as one whole line
+            if (dst >= fl + kChunk) {
+#pragma unroll
+                for (int32_t t = 0; t < kChunk; t += 16) st16v(out + fl + t, ring_ld(ring, fl + t));
+                fl += kChunk;
+            }
+        }
+    }
+    if (!slow) {  // the last partial chunk, exact bytes
+        int32_t q = fl;
+        for (; q + 16 <= pos; q += 16) st16v(out + q, ring_ld(ring, q));
+        if (q < pos) put_small(out + q, ring_ld(ring, q), (uint32_t)(pos - q));
+    }
+    if (slow) {
+        const uint32_t at = atomicAdd(&A.slow[0], 1u);
+        A.slow[1 + at] = (uint32_t)s;
+    } else {
+        A.out_size[s] = (uint64_t)pos;
+        if (A.status) A.status[s] = EZ_OK;
+    }
+}
+
+__global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *ring = smem + threadIdx.x * kRingStride;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < A.count; s += (uint64_t)gridDim.x * blockDim.x)
+        ring_one(A, s, ring);
+}
+
+}  // namespace
+
+hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t st) {
+    static bool attr_done = false;
+    const size_t lds = (size_t)kRingBlock * kRingStride;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void *)k2_ring, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        attr_done = true;
+    }
+    const uint64_t grid = (a.count + kRingBlock - 1) / kRingBlock;
+    hipLaunchKernelGGL(k2_ring, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace ez

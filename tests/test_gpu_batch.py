@@ -39,17 +39,18 @@ def _run(cuda, bufs, block=MiB, htable=1024, magic=True):
     out, sizes, status = ez.decompress_batch(packed, poff, off)
     out2, sizes2, status2 = ez.decompress_batch(packed, poff, off, exact_only=True)
     mx = int(lens.max()) if len(lens) else 0
-    out3, sizes3, status3 = ez.decompress_batch(packed, poff, off, max_len=mx)
-    ez.select_decompress_kernel("g")
-    try:
-        out4, sizes4, status4 = ez.decompress_batch(packed, poff, off, max_len=mx)
-    finally:
-        ez.select_decompress_kernel("")
+    others = [ez.decompress_batch(packed, poff, off, max_len=mx)]
+    for kind in ("f", "g"):
+        ez.select_decompress_kernel(kind)
+        try:
+            others.append(ez.decompress_batch(packed, poff, off, max_len=mx))
+        finally:
+            ez.select_decompress_kernel("")
     torch.cuda.synchronize()
-    # the lane-per-stream fast decoder, the LDS group decoder and the exact decoder agree
+    # the ring decoder (default), the lane-per-stream decoder, the LDS group decoder and the exact decoder agree
     assert torch.equal(status, status2) and torch.equal(sizes, sizes2)
     assert torch.equal(out[: int(offs[-1])], out2[: int(offs[-1])])
-    for o, z, st in ((out3, sizes3, status3), (out4, sizes4, status4)):
+    for o, z, st in others:
         assert torch.equal(st, status2) and torch.equal(z, sizes2)
         assert torch.equal(o[: int(offs[-1])], out2[: int(offs[-1])])
     return cb, packed.cpu().numpy(), poff.cpu().numpy(), out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy(), offs
