@@ -38,12 +38,12 @@ constexpr int32_t kChunk = 128;          // output leaves the ring in whole 128-
 
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 
-__device__ __forceinline__ V16 ring_ld(const uint8_t *ring, int32_t p) {
+__host__ __device__ __forceinline__ V16 ring_ld(const uint8_t *ring, int32_t p) {
     const uint8_t *q = ring + (p & (kRing - 1));
     return V16{*(const u64_ua *)q, *(const u64_ua *)(q + 8)};
 }
 // 16 bytes of output position p into the ring, keeping the mirror equal to bytes 0..15
-__device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v) {
+__host__ __device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v) {
     const int32_t r = p & (kRing - 1);
     *(u64_ua *)(ring + r) = v.lo;
     *(u64_ua *)(ring + r + 8) = v.hi;
@@ -56,7 +56,9 @@ __device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v) {
     }
 }
 
-__device__ __forceinline__ void ring_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring) {
+// decodes stream s with `ring` (kRingStride bytes) as its history; false = hand
+// the stream over (host-compilable: tools/ring_emu.hip runs it on the CPU)
+__host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring) {
     const uint8_t *b = A.in + A.in_off[s];
     const int64_t nb64 = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
     const uint8_t *in_end = A.in + A.in_off[A.count];  // loads never pass the last stream's end
@@ -173,20 +175,21 @@ __device__ __forceinline__ void ring_one(const DecompressArgs &A, const uint64_t
         for (; q + 16 <= pos; q += 16) st16v(out + q, ring_ld(ring, q));
         if (q < pos) put_small(out + q, ring_ld(ring, q), (uint32_t)(pos - q));
     }
-    if (slow) {
-        const uint32_t at = atomicAdd(&A.slow[0], 1u);
-        A.slow[1 + at] = (uint32_t)s;
-    } else {
+    if (!slow) {
         A.out_size[s] = (uint64_t)pos;
         if (A.status) A.status[s] = EZ_OK;
     }
+    return !slow;
 }
 
 __global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *ring = smem + threadIdx.x * kRingStride;
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < A.count; s += (uint64_t)gridDim.x * blockDim.x)
-        ring_one(A, s, ring);
+        if (!ring_one(A, s, ring)) {
+            const uint32_t at = atomicAdd(&A.slow[0], 1u);
+            A.slow[1 + at] = (uint32_t)s;
+        }
 }
 
 }  // namespace

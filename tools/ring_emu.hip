@@ -1,0 +1,51 @@
+// Host emulation of the K2r decoder's per-lane code (ez_decompress_ring.hip):
+// the same source, compiled for the CPU, run stream by stream.
+//   ring_emu <in.bin> <offs.bin (u64 count+1)> <cap per stream> <out.bin> <sizes.bin (u64, ~0 = handed over)>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "../eazy_amd/csrc/ez_decompress_ring.hip"
+
+static std::vector<uint8_t> slurp(const char *f) {
+    FILE *fp = std::fopen(f, "rb");
+    std::vector<uint8_t> v;
+    if (!fp) return v;
+    std::fseek(fp, 0, SEEK_END);
+    v.resize(std::ftell(fp));
+    std::fseek(fp, 0, SEEK_SET);
+    if (!v.empty() && std::fread(v.data(), 1, v.size(), fp) != v.size()) v.clear();
+    std::fclose(fp);
+    return v;
+}
+
+int main(int argc, char **argv) {
+    if (argc < 6) return 2;
+    auto in = slurp(argv[1]);
+    auto ob = slurp(argv[2]);
+    const uint64_t *offs = (const uint64_t *)ob.data();
+    const uint64_t count = ob.size() / 8 - 1, cap = (uint64_t)atoll(argv[3]);
+    std::vector<uint64_t> out_off(count + 1), size(count);
+    for (uint64_t s = 0; s <= count; s++) out_off[s] = s * cap;
+    std::vector<uint8_t> out(out_off[count] + 64);
+    std::vector<int32_t> st(count);
+    ez::DecompressArgs a{};
+    a.in = in.data();
+    a.in_off = offs;
+    a.out = out.data();
+    a.out_off = out_off.data();
+    a.out_size = size.data();
+    a.status = st.data();
+    a.count = count;
+    alignas(16) static uint8_t ring[1024];
+    for (uint64_t s = 0; s < count; s++)
+        if (!ez::ring_one(a, s, ring)) size[s] = ~0ull;
+    FILE *fo = std::fopen(argv[4], "wb");
+    for (uint64_t s = 0; s < count; s++)
+        if (size[s] != ~0ull) std::fwrite(out.data() + out_off[s], 1, size[s], fo);
+    std::fclose(fo);
+    FILE *fs = std::fopen(argv[5], "wb");
+    std::fwrite(size.data(), 8, count, fs);
+    std::fclose(fs);
+    return 0;
+}
