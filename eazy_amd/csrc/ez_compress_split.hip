@@ -158,16 +158,17 @@ __device__ __forceinline__ uint32_t row_shr(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)~0u, (int)v, 0x110 + K, 0xf, 0xf, false);
 }
 // distance to the nearest earlier lane of the group with the same hash (0: none)
-template <int K>
+// (ROW: the group is the whole 16-lane row, so a lane K below outside it reads ~0u and never matches)
+template <int K, bool ROW>
 struct Pred {
     __device__ __forceinline__ static int32_t get(uint32_t h, int lj, int32_t d) {
         const uint32_t hk = row_shr<K>(h);
-        d = (K <= lj && hk == h) ? K : d;  // descending K: the nearest one stays
-        return Pred<K - 1>::get(h, lj, d);
+        d = ((ROW || K <= lj) && hk == h) ? K : d;  // descending K: the nearest one stays
+        return Pred<K - 1, ROW>::get(h, lj, d);
     }
 };
-template <>
-struct Pred<0> {
+template <bool ROW>
+struct Pred<0, ROW> {
     __device__ __forceinline__ static int32_t get(uint32_t, int, int32_t d) { return d; }
 };
 
@@ -229,7 +230,7 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
         int32_t cand = 0;
         if constexpr (T16) {
             const int32_t tv = valid ? (int32_t)hth[h] : 0;
-            const int32_t d = Pred<G - 1>::get(h, lj, 0);
+            const int32_t d = Pred<G - 1, G == 16>::get(h, lj, 0);
             cand = d ? x - d : tv;
         } else {
             if (valid) cand = (int32_t)atomicExch(&htw[h], (uint32_t)x);

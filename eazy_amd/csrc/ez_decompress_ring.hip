@@ -182,10 +182,15 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     return !slow;
 }
 
-__global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A) {
+// spw: streams per wave (lanes spw..63 idle): fewer streams per wave put more
+// waves on each SIMD within the same LDS
+__global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A, uint32_t spw) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t *ring = smem + threadIdx.x * kRingStride;
-    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < A.count; s += (uint64_t)gridDim.x * blockDim.x)
+    const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (l >= spw) return;
+    uint8_t *ring = smem + (w * spw + l) * kRingStride;
+    const uint64_t per_block = (uint64_t)(kRingBlock / 64) * spw;
+    for (uint64_t s = (uint64_t)blockIdx.x * per_block + w * spw + l; s < A.count; s += (uint64_t)gridDim.x * per_block)
         if (!ring_one(A, s, ring)) {
             const uint32_t at = atomicAdd(&A.slow[0], 1u);
             A.slow[1 + at] = (uint32_t)s;
@@ -195,14 +200,16 @@ __global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A) {
 }  // namespace
 
 hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t st) {
+    static const uint32_t spw = getenv("EZ_K2R_SPW") ? (uint32_t)atoi(getenv("EZ_K2R_SPW")) : 64u;
     static bool attr_done = false;
-    const size_t lds = (size_t)kRingBlock * kRingStride;
+    const size_t lds = (size_t)(kRingBlock / 64) * spw * kRingStride;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k2_ring, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        (void)hipFuncSetAttribute((const void *)k2_ring, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
-    const uint64_t grid = (a.count + kRingBlock - 1) / kRingBlock;
-    hipLaunchKernelGGL(k2_ring, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a);
+    const uint64_t per_block = (uint64_t)(kRingBlock / 64) * spw;
+    const uint64_t grid = (a.count + per_block - 1) / per_block;
+    hipLaunchKernelGGL(k2_ring, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a, spw);
     return hipGetLastError();
 }
 
