@@ -12,8 +12,8 @@
 // loads, the encodes and the stores on every iteration's critical path.  Here
 //   K1p (G lanes per stream, the table in LDS) runs only the chain: visit,
 //       capped judgement, exact extension of an accepted match, the i+1
-//       insert, and one 16-byte match record per accepted match
-//       {lit_end, copy length, distance, flags} into a per-stream record slot;
+//       insert, and one 8-byte match record per accepted match
+//       {lit_end, copy length, distance, flag} into a per-stream record slot;
 //   K1e (one wave per stream) turns the records into the byte stream: token
 //       sizes, a wave prefix sum for their output positions, then every lane
 //       writes its token (literal tag, literal bytes, copy tag + offset) with
@@ -65,7 +65,12 @@ using namespace k1;
 #define EZ_PROF_MARK(k) do {} while (0)
 #endif
 
-constexpr uint32_t kRecForce = 1;    // flags: literal emitted even when empty (writeRunlen :480)
+// a match record, 8 bytes: lit_end | copy length << 20 | distance << 40 | force << 60
+// (positions < 2^20: streams <= kMaxT32); force: the literal is emitted even when
+// empty (writeRunlen :480)
+__host__ __device__ __forceinline__ uint64_t rec_pack(int32_t lit_end, int32_t clen, int32_t dist, bool force) {
+    return (uint64_t)(uint32_t)lit_end | ((uint64_t)(uint32_t)clen << 20) | ((uint64_t)(uint32_t)dist << 40) | ((uint64_t)force << 60);
+}
 constexpr int64_t kMaxT16 = 65535;   // T16 positions fit 16 bits
 constexpr int64_t kMaxT32 = 1 << 19; // the judgement packs the candidate into 20 bits (and 2n <= block)
 
@@ -174,7 +179,7 @@ struct Pred<0, ROW> {
 
 // ---------------------------------------------------------------- K1p
 template <int G, bool T16>
-__global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_words, uint4 *recs, uint64_t rcap) {
+__global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t stride_words, uint64_t *recs, uint64_t rcap) {
     constexpr int S = 64 / G;
     static_assert(!T16 || G <= 16, "T16 predecessor search works within 16-lane DPP rows");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -197,7 +202,7 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
     P.p = gp;
     P.blo = A.in;
     P.bhi = A.in + A.in_off[A.count];
-    uint4 *rec = recs + (have ? s * rcap : 0);
+    uint64_t *rec = recs + (have ? s * rcap : 0);
     // ht zero = stream position 0 (writer.go:183, A.2)
     for (int32_t k = 4 * lj; k < (int32_t)stride_words; k += 4 * G) *(uint4 *)(htw + k) = make_uint4(0, 0, 0, 0);
 
@@ -206,12 +211,9 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
     int32_t i = 0, done = 0, hiw = -1, nrec = 0;  // hiw: highest position in the table (T32)
     bool live = have && n >= 4 && !err;
     int32_t guard = 4 * n + 64;
-    // bytes x-8 .. x+23 around this lane's position x (loaded one window ahead)
-    uint64_t pxb = 0, pxf = 0, px2 = 0, px3 = 0;
-    if (live) {
-        P.around(i + lj, pxb, pxf);
-        P.around(i + lj + 16, px2, px3);
-    }
+    // bytes x-8 .. x+7 around this lane's position x (loaded one window ahead)
+    uint64_t pxb = 0, pxf = 0;
+    if (live) P.around(i + lj, pxb, pxf);
 #if (EZ_EXP & 4)
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime(), prof_it = 0;
 #endif
@@ -240,8 +242,9 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
         // ---- capped judgement (exact decision), writer.go:219-301, writeRunlen :441-463
         bool acc = false;
         int32_t info = 0;  // cand | forward count << 20 | backward count << 25 | rl << 29 | zr << 30
-        uint64_t pcb = 0, pcf = 0, pc2 = 0, pc3 = 0;
-        if (valid) {
+        uint64_t pcb = 0, pcf = 0, pc2 = 0, pc3 = 0, px2 = 0, px3 = 0;
+        if (valid) {  // x+8 .. x+23 and the candidate's bytes, in one wait
+            P.around(x + 16, px2, px3);
             P.around(cand, pcb, pcf);
             P.around(cand + 16, pc2, pc3);
         }
@@ -318,10 +321,7 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
         if (live && (err || i + 4 > n)) live = false;
         // the next window's bytes, in flight while this window's table writes and record go out
         EZ_PROF_MARK(6);
-        if (live) {
-            P.around(i + lj, pxb, pxf);
-            P.around(i + lj + 16, px2, px3);
-        }
+        if (live) P.around(i + lj, pxb, pxf);
         EZ_PROF_MARK(7);
 
         // ---- T16: the lanes Go visits store their positions (the last of a hash wins)
@@ -330,8 +330,7 @@ __global__ __launch_bounds__(64) void k1_parse(CompressArgs A, uint32_t stride_w
         }
         if (act && lj == 0) {
             if ((uint64_t)nrec < rcap)
-                rec[nrec] = make_uint4((uint32_t)lit_end, (uint32_t)(nxt - lit_end), (uint32_t)(zr ? 0 : xa - ca),
-                                       (rl && !zr) ? kRecForce : 0u);
+                rec[nrec] = rec_pack(lit_end, nxt - lit_end, zr ? 0 : xa - ca, rl && !zr);
             // the extra insert of i+1 after a window match (writer.go:315-318)
             if (!rl && xa + 1 + 4 <= n) {
                 const uint32_t h1 = a + 1 < nvalid ? h1v : ((P.u32(xa + 1) * kHashMul) >> hsh);
@@ -370,7 +369,7 @@ __device__ __forceinline__ void copy_lane(uint8_t *dst, const uint8_t *src, int3
 
 constexpr int32_t kLongLit = 96;  // literals this long are copied by the whole wave
 
-__global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint4 *recs, uint64_t rcap) {
+__global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint64_t *recs, uint64_t rcap) {
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t s = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= A.count) return;
@@ -384,7 +383,7 @@ __global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint4 *recs
     const uint64_t m64 = pr & 0xffffffffffffull;
     const int32_t m = (int32_t)(m64 < rcap ? m64 : rcap);
     int err = (int)(pr >> 48);
-    const uint4 *rec = recs + s * rcap;
+    const uint64_t *rec = recs + s * rcap;
 
     // header (writer.go:495-517): magic + reset, or reset alone
     const int32_t H = A.append_magic ? 9 : 3;
@@ -406,13 +405,13 @@ __global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint4 *recs
     for (int32_t b0 = 0; b0 < m && !full; b0 += 64) {
         const int32_t k = b0 + lane;
         const bool here = k < m;
-        const uint4 r = here ? rec[k] : make_uint4(0, 0, 0, 0);
-        const int32_t lit_end = (int32_t)r.x, clen = (int32_t)r.y, dist = (int32_t)r.z;
+        const uint64_t r = here ? rec[k] : 0ull;
+        const int32_t lit_end = (int32_t)(r & 0xfffff), clen = (int32_t)((r >> 20) & 0xfffff), dist = (int32_t)((r >> 40) & 0xfffff);
         const int32_t end = lit_end + clen;
         const int32_t prev = __shfl_up(end, 1, 64);
         const int32_t dk = lane == 0 ? done : prev;
         const int32_t L = lit_end - dk;
-        const bool lit = here && ((r.w & kRecForce) != 0 || L > 0);
+        const bool lit = here && ((r >> 60) != 0 || L > 0);
         int32_t ln = 0, tn = 0, on = 0;
         const uint64_t lb = tag_bytes(0x00, L, &ln);
         if (!lit) ln = 0;
@@ -508,7 +507,7 @@ bool split_t32_forced() {
 }
 
 template <int G, bool T16>
-hipError_t launch_split_g(const CompressArgs &a, uint4 *recs, hipStream_t st) {
+hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
         (void)hipFuncSetAttribute((const void *)k1_parse<G, T16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
@@ -524,7 +523,7 @@ hipError_t launch_split_g(const CompressArgs &a, uint4 *recs, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
-    hipLaunchKernelGGL(k1_emit, dim3(egrid), dim3(256), 0, st, a, (const uint4 *)recs, rcap);
+    hipLaunchKernelGGL(k1_emit, dim3(egrid), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
     return hipGetLastError();
 }
 
@@ -579,10 +578,10 @@ void select_split_table(bool t32) { g_split_t32 = t32; }
 
 uint32_t split_stride_words(const CompressArgs &a) { return split_table(a) != 0 ? 1u : 0u; }
 
-uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a.max_len) * 4; }
+uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a.max_len) * 2; }
 
 hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t st) {
-    uint4 *recs = (uint4 *)scratch;
+    uint64_t *recs = (uint64_t *)scratch;
     const int G = split_g(), T = split_table(a);
     if (T == 16) return G == 8 ? launch_split_g<8, true>(a, recs, st) : launch_split_g<16, true>(a, recs, st);
     return G == 8 ? launch_split_g<8, false>(a, recs, st) : launch_split_g<16, false>(a, recs, st);
