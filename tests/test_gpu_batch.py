@@ -13,10 +13,12 @@ pytestmark = pytest.mark.gpu
 MiB = 1 << 20
 
 
-@pytest.fixture(params=["", "S", "t"], ids=["auto", "split32", "tile"], autouse=True)
+@pytest.fixture(params=["", "S", "t", "r", "l", "g", "f", "w"],
+                ids=["auto", "split32", "tile", "grp", "lane", "g16", "fresh", "general"], autouse=True)
 def k1_kind(request):
     """Every batch test runs on the automatic K1 choice (K1s with the u16
-    table at these shapes), K1s with the u32 exchange table, and K1t."""
+    table at these shapes) and on every other K1 kernel forced (one that
+    cannot take a batch falls back to the automatic choice)."""
     import eazy_amd as ez
 
     ez.select_compress_kernel(request.param)
@@ -159,6 +161,6 @@ def test_split_kernel_selected(cuda, k1_kind):
     choosing them."""
     import eazy_amd as ez
 
-    want = {"": "s", "S": "s", "t": "t"}[k1_kind]
+    want = {"": "s", "S": "s"}.get(k1_kind, k1_kind)
     assert ez.compress_kernel(MiB, 1024, 4096, 65536) == want
-    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) not in "st"  # 2n > block: the general kernel
+    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) == "w"  # 2n > block: only the general kernel
