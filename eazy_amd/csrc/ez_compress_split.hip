@@ -45,6 +45,8 @@
 #include "ez_wave.h"
 #include "ez_k1_common.h"
 
+#include <type_traits>
+
 #ifndef EZ_EXP
 #define EZ_EXP 0  // diagnostic builds only: bit 2 = cycle profile of the parse loop
 #endif
@@ -87,7 +89,8 @@ __device__ __forceinline__ V16 keep_low16(V16 v, int32_t k) {
 // 16 bytes from y of the match's source side: mode 0 zeros (zero region),
 // 1 the stream itself (run length), 2 the ring image of a fresh window
 // (bytes before the stream start and from `done` on read 0)
-__device__ __forceinline__ V16 src16(const GW &P, int32_t y, int mode, int32_t done) {
+template <class SRC>
+__device__ __forceinline__ V16 src16(const SRC &P, int32_t y, int mode, int32_t done) {
     if (mode == 0) return V16{0, 0};
     uint64_t lo, hi;
     P.around(y + 8, lo, hi);  // bytes y .. y+15, zeros before the stream start
@@ -100,8 +103,8 @@ __device__ __forceinline__ V16 src16(const GW &P, int32_t y, int mode, int32_t d
 // lanes 0..G/2-1 scan forward
 // (a+k vs b+k), lanes G/2..G-1 backward (a-1-k vs b-1-k), 16 bytes per lane
 // per step, so a count below fromf + 8G bytes costs one load round trip.
-template <int G>
-__device__ __forceinline__ void gext(const GW &P, bool runf, bool runb, int g, int lj, int32_t a, int32_t b, int mode,
+template <int G, class SRC>
+__device__ __forceinline__ void gext(const SRC &P, bool runf, bool runb, int g, int lj, int32_t a, int32_t b, int mode,
                                      int32_t done, int32_t fromf, int32_t limf, int32_t limb, int32_t &resf, int32_t &resb) {
     constexpr int H = G / 2;
     constexpr uint32_t kHalf = (1u << H) - 1;
@@ -178,8 +181,10 @@ struct Pred<0, ROW> {
 };
 
 // ---------------------------------------------------------------- K1p
-template <int G, bool T16>
-__global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t stride_words, uint64_t *recs, uint64_t rcap) {
+// GIN: stream bytes read through L1/L2 (GW); else staged in LDS after the table (PW)
+template <int G, bool T16, bool GIN>
+__global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
+                                                  uint64_t rcap) {
     constexpr int S = 64 / G;
     static_assert(!T16 || G <= 16, "T16 predecessor search works within 16-lane DPP rows");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -198,13 +203,37 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
         gp = A.in + A.in_off[s];
     }
-    GW P;
-    P.p = gp;
-    P.blo = A.in;
-    P.bhi = A.in + A.in_off[A.count];
+    using SRC = typename std::conditional<GIN, GW, PW>::type;
+    SRC P;
+    if constexpr (GIN) {
+        P.p = gp;
+        P.blo = A.in;
+        P.bhi = A.in + A.in_off[A.count];
+    } else {  // [4 zero words][the stream's words][zero words to the stride's end]
+        uint32_t *pw = htw + table_words;
+        const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
+        const uint32_t r = (uint32_t)((uintptr_t)gp & 3);
+        const int32_t nw = have ? (int32_t)((r + (uint32_t)n + 3) >> 2) : 0;
+        const uint8_t *gb = gp - r;
+        P.w = pw;
+        P.pb = 16 + r;
+        for (int32_t k = lj; k < (int32_t)(stride_words - table_words); k += G) {
+            uint32_t v = 0;
+            const int32_t wk = k - 4;
+            if (wk >= 0 && wk < nw) {
+                const uint8_t *q = gb + 4 * wk;
+                if (q >= lo && q + 4 <= hi) v = *(const uint32_t *)q;
+                else
+                    for (int t = 0; t < 4; t++) v |= (q + t >= lo && q + t < hi) ? (uint32_t)q[t] << (8 * t) : 0u;
+                if (wk == 0) v &= ~0u << (8 * r);
+                v = low_bytes32(v, n - (4 * wk - (int32_t)r));
+            }
+            pw[k] = v;
+        }
+    }
     uint64_t *rec = recs + (have ? s * rcap : 0);
     // ht zero = stream position 0 (writer.go:183, A.2)
-    for (int32_t k = 4 * lj; k < (int32_t)stride_words; k += 4 * G) *(uint4 *)(htw + k) = make_uint4(0, 0, 0, 0);
+    for (int32_t k = 4 * lj; k < (int32_t)table_words; k += 4 * G) *(uint4 *)(htw + k) = make_uint4(0, 0, 0, 0);
 
     // the launcher sized records and tables from max_len: longer streams are refused
     int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : 0;
@@ -293,7 +322,7 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         EZ_PROF_MARK(2);
         const int32_t blim = zr ? ca - done : (rl ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
         int32_t fx, cx;
-        gext<G>(P, act && fk == 24, act && bk8 == 8, g, lj, fa, ca, mode, done, 24, n - fa, blim, fx, cx);
+        gext<G, SRC>(P, act && fk == 24, act && bk8 == 8, g, lj, fa, ca, mode, done, 24, n - fa, blim, fx, cx);
         const int32_t f = fk == 24 ? fx : fk;
         const int32_t c = bk8 == 8 ? cx : bk8;
         EZ_PROF_MARK(3);
@@ -485,15 +514,27 @@ __global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint64_t *r
     }
 }
 
-// LDS words per stream (0 = this variant cannot take the batch)
-template <int G, bool T16>
-uint32_t split_stride(const CompressArgs &a) {
+// LDS words of a stream's table, and of its staged input (GIN false: 4 zero
+// words, the stream, 8 zero words; 0 = this variant cannot take the batch)
+template <bool T16>
+uint32_t split_table_words(const CompressArgs &a) {
     if (a.ring || a.max_len == 0 || 2 * (int64_t)a.max_len > a.bs || a.hs > 4096 || a.hs < 4) return 0;
     if ((int64_t)a.max_len > (T16 ? kMaxT16 : kMaxT32)) return 0;
     const uint64_t words = T16 ? ((uint64_t)a.hs + 1) / 2 : (uint64_t)a.hs;
-    const uint64_t w = (words + 3) & ~3ull;
+    return (uint32_t)((words + 3) & ~3ull);
+}
+template <int G, bool T16, bool GIN>
+uint32_t split_stride(const CompressArgs &a) {
+    const uint64_t tw = split_table_words<T16>(a);
+    if (tw == 0) return 0;
+    const uint64_t w = tw + (GIN ? 0 : ((4 + (a.max_len + 3) / 4 + 8 + 3) & ~3ull));
     if (w * 4 * (64 / G) > 160 * 1024) return 0;
     return (uint32_t)w;
+}
+
+bool split_gin() {
+    static const bool v = !(getenv("EZ_K1S_GIN") && atoi(getenv("EZ_K1S_GIN")) == 0);
+    return v;
 }
 
 int split_g() {
@@ -506,20 +547,20 @@ bool split_t32_forced() {
     return v || g_split_t32;
 }
 
-template <int G, bool T16>
+template <int G, bool T16, bool GIN>
 hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_parse<G, T16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_parse<G, T16, GIN>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
     constexpr int S = 64 / G;
-    const uint32_t stride = split_stride<G, T16>(a);
+    const uint32_t stride = split_stride<G, T16, GIN>(a), tw = split_table_words<T16>(a);
     const uint64_t rcap = rec_cap(a.max_len);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
     static const size_t pad = getenv("EZ_K1S_LDSPAD") ? (size_t)atoi(getenv("EZ_K1S_LDSPAD")) : 0;
-    hipLaunchKernelGGL((k1_parse<G, T16>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, recs, rcap);
+    hipLaunchKernelGGL((k1_parse<G, T16, GIN>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
@@ -568,9 +609,9 @@ bool lds_store_in_lane_order() {
 static int split_table(const CompressArgs &a) {
     if (a.count > (1ull << 31)) return 0;
     const int G = split_g();
-    if (!split_t32_forced() && (G == 8 ? split_stride<8, true>(a) : split_stride<16, true>(a)) != 0 && lds_store_in_lane_order())
+    if (!split_t32_forced() && (G == 8 ? split_stride<8, true, true>(a) : split_stride<16, true, true>(a)) != 0 && lds_store_in_lane_order())
         return 16;
-    if ((G == 8 ? split_stride<8, false>(a) : split_stride<16, false>(a)) != 0 && lds_exchange_in_lane_order()) return 32;
+    if ((G == 8 ? split_stride<8, false, true>(a) : split_stride<16, false, true>(a)) != 0 && lds_exchange_in_lane_order()) return 32;
     return 0;
 }
 
@@ -583,8 +624,11 @@ uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a
 hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t st) {
     uint64_t *recs = (uint64_t *)scratch;
     const int G = split_g(), T = split_table(a);
-    if (T == 16) return G == 8 ? launch_split_g<8, true>(a, recs, st) : launch_split_g<16, true>(a, recs, st);
-    return G == 8 ? launch_split_g<8, false>(a, recs, st) : launch_split_g<16, false>(a, recs, st);
+    // EZ_K1S_GIN=0 (experiments): inputs staged in LDS when they fit
+    const bool lds_in = !split_gin() && (G == 8 ? split_stride<8, true, false>(a) : split_stride<16, true, false>(a)) != 0;
+    if (T == 16 && lds_in) return G == 8 ? launch_split_g<8, true, false>(a, recs, st) : launch_split_g<16, true, false>(a, recs, st);
+    if (T == 16) return G == 8 ? launch_split_g<8, true, true>(a, recs, st) : launch_split_g<16, true, true>(a, recs, st);
+    return G == 8 ? launch_split_g<8, false, true>(a, recs, st) : launch_split_g<16, false, true>(a, recs, st);
 }
 
 }  // namespace ez
