@@ -30,6 +30,7 @@
 #include "ez_format.h"
 #include "ez_internal.h"
 #include "ez_wave.h"
+#include "ez_bytes.h"
 
 #include <stdlib.h>
 
@@ -179,6 +180,24 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         return 0u;
     };
 
+    // 8 stream bytes from y (global view; any bytes outside the batch read 0),
+    // and the 8 bytes block[(y .. y+7) & mask] when they map to 8 consecutive stream
+    // bytes or to the zero history before a fresh stream (false: take the byte loop)
+    const uint8_t *in_lo = A.in, *in_hi = A.in + A.in_off[A.count];
+    auto s8 = [&](int64_t y) -> uint64_t {
+        const uint8_t *q = P.g + y;
+        if (q >= in_lo && q + 8 <= in_hi) return *(const uint64_t __attribute__((aligned(1))) *)q;
+        return (in_hi - in_lo >= 16) ? ld_clamped(q, in_lo, in_hi).lo : 0ull;
+    };
+    auto ring8 = [&](int64_t y, int64_t wpos, uint64_t &v) -> bool {
+        const int64_t r = (y - wpos) & mask;
+        if (r + 7 >= bs) return false;  // wraps inside the 8 bytes
+        const int64_t q = wpos - bs + r;
+        if (q >= start) { v = s8(q - start); return true; }
+        if (!RING && q + 8 <= start) { v = 0; return true; }
+        return false;
+    };
+
     int64_t done = 0, i = 0;
     int64_t guard = 0;
     const int64_t guard_max = 16 * n + 4096;
@@ -234,10 +253,18 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 if (st + 8 < n && P.u32(st) == 0 && P.u32(st + 4) == 0) {
                     kind = kZero;
                 } else {
-                    int f = 0;
-                    while (f < kCap && x + f < n && P.b(st + f) == P.b(x + f)) f++;
-                    int c = 0;
-                    while (c < kCap && st - 1 - c >= 0 && x - 1 - c >= done && P.b(st - 1 - c) == P.b(x - 1 - c)) c++;
+                    int f = 0, c = 0;
+                    if (!PL && kCap == 8) {  // 8-byte compares (writeRunlen :449-462, capped)
+                        const uint64_t df = s8(st) ^ s8(x), db = s8(st - 8) ^ s8(x - 8);
+                        f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
+                        if (f > n - x) f = (int)(n - x);
+                        c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
+                        const int64_t cl = st < x - done ? st : x - done;
+                        if (c > cl) c = (int)cl;
+                    } else {
+                        while (f < kCap && x + f < n && P.b(st + f) == P.b(x + f)) f++;
+                        while (c < kCap && st - 1 - c >= 0 && x - 1 - c >= done && P.b(st - 1 - c) == P.b(x - 1 - c)) c++;
+                    }
                     const bool capped = f == kCap || c == kCap;
                     if (!capped && f + c < kMinCopyChunk) kind = kReject;
                     else if (x - st >= bs - 8) kind = kCut;
@@ -247,11 +274,29 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 // window match (writer.go:233-301)
                 int64_t ist = x - 1, st = cand - 1;
                 int c = 0;
-                while (c < kCap && ist >= done && P.b(ist) == ringb(st, wpos)) { ist--; st--; c++; }
+                uint64_t rb, rf;
+                const bool vec = !PL && kCap == 8 && ring8(cand - 8, wpos, rb) && ring8(cand, wpos, rf);
+                if (vec) {  // 8-byte compares against the ring image (writer.go:236-259, capped)
+                    const uint64_t db = s8(x - 8) ^ rb;
+                    c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
+                    if (c > x - done) c = (int)(x - done);
+                    ist -= c;
+                    st -= c;
+                } else {
+                    while (c < kCap && ist >= done && P.b(ist) == ringb(st, wpos)) { ist--; st--; c++; }
+                }
                 ist++; st++;
                 int64_t iend = x, end = cand;
                 int f = 0;
-                while (f < kCap && iend < n && P.b(iend) == ringb(end, wpos)) { iend++; end++; f++; }
+                if (vec) {
+                    const uint64_t df = s8(x) ^ rf;
+                    f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
+                    if (f > n - x) f = (int)(n - x);
+                    iend += f;
+                    end += f;
+                } else {
+                    while (f < kCap && iend < n && P.b(iend) == ringb(end, wpos)) { iend++; end++; f++; }
+                }
                 const bool capped = c == kCap || f == kCap;
                 const int64_t blit = wpos - bs;
                 const int64_t bend = blit + (iend - done);
