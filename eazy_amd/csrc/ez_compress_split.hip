@@ -359,7 +359,8 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         }
         if (act && lj == 0) {
             if ((uint64_t)nrec < rcap)
-                rec[nrec] = rec_pack(lit_end, nxt - lit_end, zr ? 0 : xa - ca, rl && !zr);
+                // non-temporal: the records must not evict the streams' inputs from L2
+                __builtin_nontemporal_store(rec_pack(lit_end, nxt - lit_end, zr ? 0 : xa - ca, rl && !zr), rec + nrec);
             // the extra insert of i+1 after a window match (writer.go:315-318)
             if (!rl && xa + 1 + 4 <= n) {
                 const uint32_t h1 = a + 1 < nvalid ? h1v : ((P.u32(xa + 1) * kHashMul) >> hsh);

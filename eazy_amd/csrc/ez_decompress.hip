@@ -408,7 +408,8 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     // long streams (slots of 64 KiB and more, C2/C4): a lane per stream moves 16 bytes per
     // dependent step and few streams fill few lanes; the wave-per-stream decoder moves 64
     static const bool use_exact = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "exact") == 0;
-    if (use_exact || a.max_out >= (64u << 10)) {
+    static const uint64_t long_slot = getenv("EZ_K2_LONG") ? (uint64_t)atoll(getenv("EZ_K2_LONG")) : (64u << 10);
+    if (use_exact || a.max_out >= long_slot) {
         DecompressArgs b = a;
         b.slow = nullptr;
         uint64_t grid = b.count < (1u << 30) ? b.count : (1u << 30);
