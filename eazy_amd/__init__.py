@@ -491,6 +491,39 @@ def compress_batch(data, in_off, block: int = MiB, htable: int = 1024, max_len: 
     return out
 
 
+def compress_batch_writes(data, in_off, write_idx, write_end, block: int = MiB, htable: int = 1024,
+                          append_magic: bool = True, stream=None) -> CompressedBatch:
+    """K1 for multi-Write streams: stream s receives the Writes k = write_idx[s]
+    .. write_idx[s+1]-1, Write k ending at data[write_end[k]] (CUDA int64 tensors).
+    Its slot holds the bytes Go's sink receives over those Write calls."""
+    import torch
+
+    _need_cuda(data, in_off, write_idx, write_end)
+    count = in_off.numel() - 1
+    nw = write_idx[1:] - write_idx[:-1]
+    n = in_off[1:] - in_off[:-1]
+    cap = (n + (n >> 2) + 32 + 5 * nw + 15) & ~15  # ez_compress_bound + a trailing literal tag per Write
+    slot_off = torch.cat([torch.zeros(1, dtype=torch.int64, device=data.device), torch.cumsum(cap, 0)])
+    total = int(slot_off[-1].item())
+    out = CompressedBatch(
+        torch.empty(total + 16, dtype=torch.uint8, device=data.device),
+        slot_off,
+        torch.empty(count, dtype=torch.int64, device=data.device),
+        torch.empty(count, dtype=torch.int32, device=data.device),
+    )
+    max_len = int((in_off[1:] - in_off[:-1]).max().item()) if count else 0
+    max_writes = int(nw.max().item()) if count else 1
+    b = _Batch(data.data_ptr(), in_off.data_ptr(), out.slots.data_ptr(), out.slot_off.data_ptr(),
+               out.sizes.data_ptr(), out.status.data_ptr(), count, max_len)
+    L = _lib()
+    L.ez_compress_batch_writes.argtypes = [C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64,
+                                           C.c_void_p]
+    flags = 0 if append_magic else F_NO_MAGIC
+    _check(L.ez_compress_batch_writes(block, htable, flags, C.byref(b), write_idx.data_ptr(), write_end.data_ptr(),
+                                      max(1, max_writes), _stream_ptr(stream)))
+    return out
+
+
 def pack(cb: CompressedBatch, packed=None, packed_off=None, workspace=None, stream=None):
     """K3: dense packing of the compressed slots -> (packed, packed_off)."""
     import torch

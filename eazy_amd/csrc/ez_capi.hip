@@ -464,7 +464,8 @@ extern "C" int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size
 
 // ------------------------------------------------------------------ batches
 
-extern "C" int ez_compress_batch(int64_t block, int64_t htable, int flags, const ez_batch *b, void *hip_stream) {
+static int compress_batch_impl(int64_t block, int64_t htable, int flags, const ez_batch *b, const uint64_t *write_idx,
+                               const uint64_t *write_end, uint64_t max_writes, void *hip_stream) {
     if (!valid_writer_sizes(block, htable)) return EZ_EINVAL;
     if (device_count() <= 0) return EZ_EDEVICE;
     ez::CompressArgs a{};
@@ -483,7 +484,12 @@ extern "C" int ez_compress_batch(int64_t block, int64_t htable, int flags, const
     a.start = 0;
     a.ring = nullptr;
     a.max_len = b->max_len;
-    const uint64_t words = ez::compress_scratch_words(a);
+    a.write_idx = write_idx;
+    a.write_end = write_end;
+    a.max_writes = max_writes;
+    // multi-Write streams run on K1s only (fresh streams, 2 x stream <= block)
+    if (write_idx && (b->count == 0 || ez::split_stride_words(a) == 0)) return b->count == 0 ? EZ_OK : EZ_EINVAL;
+    const uint64_t words = write_idx ? ez::split_scratch_words(a) : ez::compress_scratch_words(a);
     if (words) {
         int dev = 0;
         EZ_HIP(hipGetDevice(&dev));
@@ -492,8 +498,19 @@ extern "C" int ez_compress_batch(int64_t block, int64_t htable, int flags, const
         if (g_scratch[(size_t)dev].ht.ensure((size_t)words * 4)) return EZ_EDEVICE;
         a.ht_global = g_scratch[(size_t)dev].ht.as<uint32_t>();
     }
-    EZ_HIP(ez::launch_compress(a, (hipStream_t)hip_stream));
+    if (write_idx) EZ_HIP(ez::launch_compress_split(a, a.ht_global, (hipStream_t)hip_stream));
+    else EZ_HIP(ez::launch_compress(a, (hipStream_t)hip_stream));
     return EZ_OK;
+}
+
+extern "C" int ez_compress_batch(int64_t block, int64_t htable, int flags, const ez_batch *b, void *hip_stream) {
+    return compress_batch_impl(block, htable, flags, b, nullptr, nullptr, 0, hip_stream);
+}
+
+extern "C" int ez_compress_batch_writes(int64_t block, int64_t htable, int flags, const ez_batch *b, const uint64_t *write_idx,
+                                        const uint64_t *write_end, uint64_t max_writes, void *hip_stream) {
+    if (!write_idx || !write_end || max_writes == 0) return EZ_EINVAL;
+    return compress_batch_impl(block, htable, flags, b, write_idx, write_end, max_writes, hip_stream);
 }
 
 extern "C" size_t ez_pack_workspace(uint64_t count) { return ez::pack_workspace(count); }

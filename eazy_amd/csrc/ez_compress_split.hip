@@ -76,8 +76,11 @@ __host__ __device__ __forceinline__ uint64_t rec_pack(int32_t lit_end, int32_t c
 constexpr int64_t kMaxT16 = 65535;   // T16 positions fit 16 bits
 constexpr int64_t kMaxT32 = 1 << 19; // the judgement packs the candidate into 20 bits (and 2n <= block)
 
-// record slot of stream s: s * rec_cap .. ; rec_cap = max_len / 6 + 1
-__host__ __device__ __forceinline__ uint64_t rec_cap(uint64_t max_len) { return max_len / 6 + 1; }
+// record slot of stream s: s * rec_cap .. ; every match advances done by >= 6,
+// and every Write but the last ends with a marker record
+__host__ __device__ __forceinline__ uint64_t rec_cap(const CompressArgs &a) {
+    return a.max_len / 6 + 1 + (a.write_idx ? a.max_writes : 0);
+}
 
 // bytes [0, k) of v kept, the rest 0 (k <= 0: none, k >= 16: all)
 __device__ __forceinline__ V16 keep_low16(V16 v, int32_t k) {
@@ -182,7 +185,8 @@ struct Pred<0, ROW> {
 
 // ---------------------------------------------------------------- K1p
 // GIN: stream bytes read through L1/L2 (GW); else staged in LDS after the table (PW)
-template <int G, bool T16, bool GIN>
+// MW: streams of several Writes (CompressArgs::write_idx), else one Write each
+template <int G, bool T16, bool GIN, bool MW>
 __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                   uint64_t rcap) {
     constexpr int S = 64 / G;
@@ -238,8 +242,18 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
     // the launcher sized records and tables from max_len: longer streams are refused
     int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : 0;
     int32_t i = 0, done = 0, hiw = -1, nrec = 0;  // hiw: highest position in the table (T32)
-    bool live = have && n >= 4 && !err;
-    int32_t guard = 4 * n + 64;
+    // Writes of the stream (writer.go:206: each Write's loop runs to its own len(p)):
+    // wend = the current Write's end, wk / wlast = its index / the last one's
+    uint64_t wk = 0, wlast = 0;
+    int32_t wend = n, wstart = 0;
+    if (MW && have) {
+        wk = A.write_idx[s];
+        wlast = A.write_idx[s + 1] - 1;
+        if (A.write_idx[s + 1] <= wk) err = EZ_EINVAL;
+        else wend = (int32_t)(A.write_end[wk] - A.in_off[s]);
+    }
+    bool live = have && !err && (n >= 4 || wk < wlast);
+    int32_t guard = 4 * n + 64 + 2 * (int32_t)(wlast - wk);
     // bytes x-8 .. x+7 around this lane's position x (loaded one window ahead)
     uint64_t pxb = 0, pxf = 0;
     if (live) P.around(i + lj, pxb, pxf);
@@ -251,7 +265,19 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         prof_it++;
 #endif
         if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
-        int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
+        // a Write that has no position left ends (its trailing literal, writer.go:324-329, is
+        // the emitter's: a marker record), and the next Write starts where it ended
+        while (MW && live && i + 4 > wend && wk < wlast) {
+            if (lj == 0 && (uint64_t)nrec < rcap) __builtin_nontemporal_store(rec_pack(wend, 0, 0, false), rec + nrec);
+            if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
+            nrec++;
+            i = done = wstart = wend;
+            wk++;
+            wend = (int32_t)(A.write_end[wk] - A.in_off[s]);
+            if (live) P.around(i + lj, pxb, pxf);
+        }
+        if (live && i + 4 > wend) live = false;  // the last Write has no position left
+        int32_t nvalid = wend - 3 - i < G ? wend - 3 - i : G;
         if (!T16 && i <= hiw) nvalid = 1;  // T32, not monotone: one position per window
         const int32_t x = i + lj;
         const bool valid = live && lj < nvalid;
@@ -280,8 +306,9 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         EZ_PROF_MARK(5);
         if (valid) {
             const bool rl = cand >= done && cand < x;
-            const bool zr = rl && cand + 8 < n && pcf == 0;
-            const int32_t bl = rl ? ((x - done) < cand ? (x - done) : cand) : x - done;
+            const bool zr = rl && cand + 8 < wend && pcf == 0;
+            // writeRunlen's backward scan stays inside this Write's p (st+jb >= 0, writer.go:458)
+            const int32_t bl = rl ? ((x - done) < cand - wstart ? (x - done) : cand - wstart) : x - done;
             int32_t jb = clz_bytes(pxb ^ pcb);
             jb = jb < bl ? jb : bl;
             // forward, 24 bytes capped; the window branch compares the ring image (0 from done on)
@@ -290,13 +317,13 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
             const uint64_t d0 = pxf ^ (rl ? pcf : low_bytes(pcf, done - cand));
             const uint64_t d1 = px2 ^ c2.lo, d2 = px3 ^ c2.hi;
             int32_t jf = d0 ? ctz_bytes(d0) : (d1 ? 8 + ctz_bytes(d1) : 16 + ctz_bytes(d2));
-            jf = jf < n - x ? jf : n - x;
+            jf = jf < wend - x ? jf : wend - x;
             acc = rl ? (zr || jf + jb >= kMinCopyChunk) : ((jf < done - cand ? jf : done - cand) + jb >= kMinCopyChunk);
             int32_t zb = clz_bytes(pcb);
             zb = zb < cand - done ? zb : cand - done;
             // zero region: the zeros from cand on, 24 bytes capped
             int32_t zf = pc2 ? 8 + ctz_bytes(pc2) : 16 + ctz_bytes(pc3);
-            zf = zf < n - cand ? zf : n - cand;
+            zf = zf < wend - cand ? zf : wend - cand;
             const int32_t fk = zr ? zf : jf, bk = zr ? zb : jb;
             info = cand | (fk << 20) | (bk << 25) | ((int32_t)rl << 29) | ((int32_t)zr << 30);
         }
@@ -320,9 +347,9 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         const int mode = zr ? 0 : (rl ? 1 : 2);
         const int32_t fa = zr ? ca : xa;
         EZ_PROF_MARK(2);
-        const int32_t blim = zr ? ca - done : (rl ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
+        const int32_t blim = zr ? ca - done : (rl ? ((xa - done) < ca - wstart ? (xa - done) : ca - wstart) : xa - done);
         int32_t fx, cx;
-        gext<G, SRC>(P, act && fk == 24, act && bk8 == 8, g, lj, fa, ca, mode, done, 24, n - fa, blim, fx, cx);
+        gext<G, SRC>(P, act && fk == 24, act && bk8 == 8, g, lj, fa, ca, mode, done, 24, wend - fa, blim, fx, cx);
         const int32_t f = fk == 24 ? fx : fk;
         const int32_t c = bk8 == 8 ? cx : bk8;
         EZ_PROF_MARK(3);
@@ -347,7 +374,7 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
             hiw = hiw > top ? hiw : top;
             i += nvalid;
         }
-        if (live && (err || i + 4 > n)) live = false;
+        if (live && (err || (i + 4 > wend && wk == wlast))) live = false;
         // the next window's bytes, in flight while this window's table writes and record go out
         EZ_PROF_MARK(6);
         if (live) P.around(i + lj, pxb, pxf);
@@ -362,7 +389,7 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
                 // non-temporal: the records must not evict the streams' inputs from L2
                 __builtin_nontemporal_store(rec_pack(lit_end, nxt - lit_end, zr ? 0 : xa - ca, rl && !zr), rec + nrec);
             // the extra insert of i+1 after a window match (writer.go:315-318)
-            if (!rl && xa + 1 + 4 <= n) {
+            if (!rl && xa + 1 + 4 <= wend) {
                 const uint32_t h1 = a + 1 < nvalid ? h1v : ((P.u32(xa + 1) * kHashMul) >> hsh);
                 if constexpr (T16) hth[h1] = (uint16_t)(xa + 1);
                 else htw[h1] = (uint32_t)(xa + 1);
@@ -445,8 +472,12 @@ __global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint64_t *r
         int32_t ln = 0, tn = 0, on = 0;
         const uint64_t lb = tag_bytes(0x00, L, &ln);
         if (!lit) ln = 0;
-        const uint64_t tb = tag_bytes(0x80, clen, &tn);
-        const uint64_t ob = off_bytes(dist, clen, &on);
+        uint64_t tb = tag_bytes(0x80, clen, &tn);
+        uint64_t ob = off_bytes(dist, clen, &on);
+        if (clen == 0) {  // a Write's end: its trailing literal only (writer.go:324-329)
+            tb = ob = 0;
+            tn = on = 0;
+        }
         const int32_t T = here ? ln + (lit ? L : 0) + tn + on : 0;
         // inclusive prefix sum of T over the wave
         int32_t incl = T;
@@ -468,9 +499,11 @@ __global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint64_t *r
                 if (L >= kLongLit) longlit = true;
                 else copy_lane(d + ln, p + dk, L, lo, hi);
             }
-            const uint64_t c0 = tb | (ob << (8 * tn));
-            const uint64_t c1 = ob >> (64 - 8 * tn);  // tn >= 1
-            put_small(d + T - tn - on, V16{c0, c1}, (uint32_t)(tn + on));
+            if (tn) {
+                const uint64_t c0 = tb | (ob << (8 * tn));
+                const uint64_t c1 = ob >> (64 - 8 * tn);
+                put_small(d + T - tn - on, V16{c0, c1}, (uint32_t)(tn + on));
+            }
         }
         // long literals: the whole wave, one at a time
         for (uint64_t lm = __ballot(longlit); lm; lm &= lm - 1) {
@@ -548,20 +581,20 @@ bool split_t32_forced() {
     return v || g_split_t32;
 }
 
-template <int G, bool T16, bool GIN>
+template <int G, bool T16, bool GIN, bool MW>
 hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_parse<G, T16, GIN>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_parse<G, T16, GIN, MW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
     constexpr int S = 64 / G;
     const uint32_t stride = split_stride<G, T16, GIN>(a), tw = split_table_words<T16>(a);
-    const uint64_t rcap = rec_cap(a.max_len);
+    const uint64_t rcap = rec_cap(a);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
     static const size_t pad = getenv("EZ_K1S_LDSPAD") ? (size_t)atoi(getenv("EZ_K1S_LDSPAD")) : 0;
-    hipLaunchKernelGGL((k1_parse<G, T16, GIN>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap);
+    hipLaunchKernelGGL((k1_parse<G, T16, GIN, MW>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
@@ -620,16 +653,20 @@ void select_split_table(bool t32) { g_split_t32 = t32; }
 
 uint32_t split_stride_words(const CompressArgs &a) { return split_table(a) != 0 ? 1u : 0u; }
 
-uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a.max_len) * 2; }
+uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a) * 2; }
 
 hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t st) {
     uint64_t *recs = (uint64_t *)scratch;
     const int G = split_g(), T = split_table(a);
+    if (a.write_idx) {  // multi-Write streams: inputs through L1/L2
+        if (T == 16) return G == 8 ? launch_split_g<8, true, true, true>(a, recs, st) : launch_split_g<16, true, true, true>(a, recs, st);
+        return G == 8 ? launch_split_g<8, false, true, true>(a, recs, st) : launch_split_g<16, false, true, true>(a, recs, st);
+    }
     // EZ_K1S_GIN=0 (experiments): inputs staged in LDS when they fit
     const bool lds_in = !split_gin() && (G == 8 ? split_stride<8, true, false>(a) : split_stride<16, true, false>(a)) != 0;
-    if (T == 16 && lds_in) return G == 8 ? launch_split_g<8, true, false>(a, recs, st) : launch_split_g<16, true, false>(a, recs, st);
-    if (T == 16) return G == 8 ? launch_split_g<8, true, true>(a, recs, st) : launch_split_g<16, true, true>(a, recs, st);
-    return G == 8 ? launch_split_g<8, false, true>(a, recs, st) : launch_split_g<16, false, true>(a, recs, st);
+    if (T == 16 && lds_in) return G == 8 ? launch_split_g<8, true, false, false>(a, recs, st) : launch_split_g<16, true, false, false>(a, recs, st);
+    if (T == 16) return G == 8 ? launch_split_g<8, true, true, false>(a, recs, st) : launch_split_g<16, true, true, false>(a, recs, st);
+    return G == 8 ? launch_split_g<8, false, true, false>(a, recs, st) : launch_split_g<16, false, true, false>(a, recs, st);
 }
 
 }  // namespace ez

@@ -27,6 +27,11 @@ struct CompressArgs {
     uint8_t *ring;            // the handle's ring (block), updated in place; nullptr = fresh stream
     uint32_t *ht_global;      // persistent hash table (handle) / per-block scratch (large hs)
     uint64_t max_len;         // max stream length (0 = unknown)
+    // batch of multi-Write streams (nullptr = one Write per stream): stream s receives
+    // the Writes k = write_idx[s] .. write_idx[s+1]-1, Write k ending at in[write_end[k]]
+    const uint64_t *write_idx;
+    const uint64_t *write_end;
+    uint64_t max_writes;      // the most Writes of one stream (records reserved for their ends)
 };
 
 // One K2 launch.  Batch: count complete streams from fresh Readers.

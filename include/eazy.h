@@ -142,6 +142,16 @@ typedef struct {
 
 /* K1: compress every stream of b into its slot (slot >= ez_compress_bound(n)). */
 int ez_compress_batch(int64_t block, int64_t htable, int flags, const ez_batch *b, void *hip_stream);
+/* K1 for streams that each receive several Writes (Writer.Write writer.go:206
+ * called k times on one NewWriter, FlushThreshold 0: the slot holds what the
+ * sink receives over the k calls).  Stream s receives the Writes
+ * k = write_idx[s] .. write_idx[s+1]-1 (device arrays, write_idx[count+1]);
+ * Write k is in[prev .. write_end[k]) with prev = in_off[s] for the first.
+ * max_writes: the most Writes of one stream (host hint).  Slots need
+ * ez_compress_bound(n) + 5 bytes per Write.  Fresh streams with 2 x length
+ * <= block only (the K1s regime); otherwise EZ_EINVAL. */
+int ez_compress_batch_writes(int64_t block, int64_t htable, int flags, const ez_batch *b, const uint64_t *write_idx,
+                             const uint64_t *write_end, uint64_t max_writes, void *hip_stream);
 /* K3: exclusive scan of sizes -> packed_off[count+1], then gather the slots
  * densely into packed.  workspace >= ez_pack_workspace(count) device bytes. */
 size_t ez_pack_workspace(uint64_t count);

@@ -164,3 +164,50 @@ def test_split_kernel_selected(cuda, k1_kind):
     want = {"": "s", "S": "s"}.get(k1_kind, k1_kind)
     assert ez.compress_kernel(MiB, 1024, 4096, 65536) == want
     assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) == "w"  # 2n > block: only the general kernel
+
+
+def test_multi_write_streams(cuda, k1_kind):
+    """Streams that each receive several Writes (one NewWriter, k calls of
+    Write, FlushThreshold 0): the slot holds the bytes the sink
+    receives over the k calls, equal to the oracle's for the same Writes —
+    ragged Writes, empty ones, ones shorter than a hash (4 bytes), one Write."""
+    if k1_kind:
+        pytest.skip("multi-Write batches run on the automatic K1s choice")
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(21)
+    d = synth.logs(23, 1 << 20).tobytes()
+    streams, at = [], 0
+    for s in range(96):
+        k = int(rng.integers(1, 9))
+        ws = []
+        for _ in range(k):
+            n = int(rng.choice([0, 1, 3, 4, 5, 17, int(rng.integers(0, 3000))]))
+            ws.append(d[at : at + n])
+            at += n
+        streams.append(ws)
+    data = b"".join(b"".join(ws) for ws in streams)
+    in_off, w_idx, w_end = [0], [0], []
+    pos = 0
+    for ws in streams:
+        for w in ws:
+            pos += len(w)
+            w_end.append(pos)
+        in_off.append(pos)
+        w_idx.append(len(w_end))
+    dev = cuda
+    t = lambda a: torch.tensor(a, dtype=torch.int64, device=dev)
+    host = np.frombuffer(data, np.uint8)
+    dd = torch.from_numpy(host.copy()).to(dev) if len(host) else torch.zeros(1, dtype=torch.uint8, device=dev)
+    cb = ez.compress_batch_writes(dd, t(in_off), t(w_idx), t(w_end), MiB, 1024)
+    torch.cuda.synchronize()
+    st, sz, so = cb.status.cpu().numpy(), cb.sizes.cpu().numpy(), cb.slot_off.cpu().numpy()
+    slots = cb.slots.cpu().numpy()
+    for s, ws in enumerate(streams):
+        assert st[s] == 0, (s, st[s])
+        want = orc.compress(MiB, 1024, ws)
+        got = slots[so[s] : so[s] + sz[s]].tobytes()
+        assert got == want, f"stream {s}: {len(ws)} Writes of {[len(w) for w in ws]}"
