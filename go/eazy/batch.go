@@ -14,28 +14,54 @@ import (
 	"unsafe"
 )
 
-// compressBatch stages the buffers into device memory, runs K1 (one stream
-// per buffer) and copies every slot back.  One HIP stream per call.
+// compressBatch: one stream per buffer (one Write each).
 func compressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
-	count := len(bufs)
+	streams := make([][][]byte, len(bufs))
+	for k, b := range bufs {
+		streams[k] = [][]byte{b}
+	}
+	return compressStreams(streams, block, htable)
+}
+
+// compressStreams stages the streams into device memory, runs K1 (stream k =
+// NewWriter(block, htable) receiving the Writes streams[k] in order,
+// FlushThreshold 0) and copies every slot back.  One HIP stream per call.
+func compressStreams(streams [][][]byte, block, htable int) ([][]byte, error) {
+	count := len(streams)
 	if count == 0 {
 		return nil, nil
 	}
 	inOff := make([]uint64, count+1)
 	outOff := make([]uint64, count+1)
-	maxLen := 0
-	for k, b := range bufs {
-		inOff[k+1] = inOff[k] + uint64(len(b))
-		outOff[k+1] = outOff[k] + uint64(C.ez_compress_bound(C.size_t(len(b))))
-		if len(b) > maxLen {
-			maxLen = len(b)
+	writeIdx := make([]uint64, count+1)
+	var writeEnd []uint64
+	maxLen, maxWrites, multi := 0, 1, false
+	for k, ws := range streams {
+		n := 0
+		for _, w := range ws {
+			n += len(w)
+			writeEnd = append(writeEnd, inOff[k]+uint64(n))
+		}
+		if len(ws) != 1 {
+			multi = true
+		}
+		if len(ws) > maxWrites {
+			maxWrites = len(ws)
+		}
+		inOff[k+1] = inOff[k] + uint64(n)
+		writeIdx[k+1] = uint64(len(writeEnd))
+		outOff[k+1] = outOff[k] + uint64(C.ez_compress_bound(C.size_t(n))) + 5*uint64(len(ws))
+		if n > maxLen {
+			maxLen = n
 		}
 	}
 	host := make([]byte, 0, inOff[count])
-	for _, b := range bufs {
-		host = append(host, b...)
+	for _, ws := range streams {
+		for _, w := range ws {
+			host = append(host, w...)
+		}
 	}
-	var dIn, dOut, dInOff, dOutOff, dSize, dStatus unsafe.Pointer
+	var dIn, dOut, dInOff, dOutOff, dSize, dStatus, dWIdx, dWEnd unsafe.Pointer
 	alloc := func(p *unsafe.Pointer, n uint64) error {
 		if C.hipMalloc(p, C.size_t(n+16)) != C.hipSuccess {
 			return ErrDevice
@@ -43,7 +69,7 @@ func compressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
 		return nil
 	}
 	defer func() {
-		for _, p := range []unsafe.Pointer{dIn, dOut, dInOff, dOutOff, dSize, dStatus} {
+		for _, p := range []unsafe.Pointer{dIn, dOut, dInOff, dOutOff, dSize, dStatus, dWIdx, dWEnd} {
 			if p != nil {
 				C.hipFree(p)
 			}
@@ -53,7 +79,8 @@ func compressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
 		p *unsafe.Pointer
 		n uint64
 	}{{&dIn, inOff[count]}, {&dOut, outOff[count]}, {&dInOff, 8 * uint64(count+1)}, {&dOutOff, 8 * uint64(count+1)},
-		{&dSize, 8 * uint64(count)}, {&dStatus, 4 * uint64(count)}} {
+		{&dSize, 8 * uint64(count)}, {&dStatus, 4 * uint64(count)}, {&dWIdx, 8 * uint64(count+1)},
+		{&dWEnd, 8 * uint64(len(writeEnd))}} {
 		if err := alloc(a.p, a.n); err != nil {
 			return nil, err
 		}
@@ -67,7 +94,18 @@ func compressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
 		in: (*C.uint8_t)(dIn), in_off: (*C.uint64_t)(dInOff), out: (*C.uint8_t)(dOut), out_off: (*C.uint64_t)(dOutOff),
 		out_size: (*C.uint64_t)(dSize), status: (*C.int32_t)(dStatus), count: C.uint64_t(count), max_len: C.uint64_t(maxLen),
 	}
-	if st := C.ez_compress_batch(C.int64_t(block), C.int64_t(htable), 0, &b, nil); st != C.EZ_OK {
+	var st C.int
+	if multi {
+		C.hipMemcpy(dWIdx, unsafe.Pointer(&writeIdx[0]), C.size_t(8*(count+1)), C.hipMemcpyHostToDevice)
+		if len(writeEnd) > 0 {
+			C.hipMemcpy(dWEnd, unsafe.Pointer(&writeEnd[0]), C.size_t(8*len(writeEnd)), C.hipMemcpyHostToDevice)
+		}
+		st = C.ez_compress_batch_writes(C.int64_t(block), C.int64_t(htable), 0, &b, (*C.uint64_t)(dWIdx),
+			(*C.uint64_t)(dWEnd), C.uint64_t(maxWrites), nil)
+	} else {
+		st = C.ez_compress_batch(C.int64_t(block), C.int64_t(htable), 0, &b, nil)
+	}
+	if st != C.EZ_OK {
 		return nil, toErr(st, 0)
 	}
 	out := make([]byte, outOff[count])
@@ -77,7 +115,7 @@ func compressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
 	C.hipMemcpy(unsafe.Pointer(&size[0]), dSize, C.size_t(8*count), C.hipMemcpyDeviceToHost)
 	C.hipMemcpy(unsafe.Pointer(&status[0]), dStatus, C.size_t(4*count), C.hipMemcpyDeviceToHost)
 	res := make([][]byte, count)
-	for k := range bufs {
+	for k := range streams {
 		if status[k] != 0 {
 			return nil, errors.Join(ErrDevice, toErr(C.int(status[k]), 0))
 		}

@@ -359,3 +359,11 @@ func (r *Reader) more() error { // reader.go:516-543
 func CompressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
 	return compressBatch(bufs, block, htable) // batch.go
 }
+
+// CompressStreams is the multi-Write batch (Go-only extension): stream k is a
+// fresh NewWriter(block, htable) receiving streams[k][0], streams[k][1], ...
+// through Write with FlushThreshold 0; the result is what its sink receives.
+// Streams with 2 x total length > block are refused (EINVAL).
+func CompressStreams(streams [][][]byte, block, htable int) ([][]byte, error) {
+	return compressStreams(streams, block, htable) // batch.go
+}
