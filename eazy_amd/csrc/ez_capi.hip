@@ -9,6 +9,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -96,11 +97,12 @@ size_t header_bytes(uint8_t *b, int append_magic, int ver, int64_t bs) {
     return k;
 }
 
-// per-device scratch for batch compression with large hash tables
+// K1 scratch (match records / global hash tables), one per (device, HIP stream):
+// batch calls on distinct streams may run concurrently (SURVEY §8b threading)
 struct Scratch {
     DBuf ht;
 };
-std::vector<Scratch> g_scratch;
+std::map<std::pair<int, void *>, Scratch> g_scratch;
 
 }  // namespace
 
@@ -494,9 +496,9 @@ static int compress_batch_impl(int64_t block, int64_t htable, int flags, const e
         int dev = 0;
         EZ_HIP(hipGetDevice(&dev));
         std::lock_guard<std::mutex> lk(g_mu);
-        if ((int)g_scratch.size() <= dev) g_scratch.resize((size_t)dev + 1);
-        if (g_scratch[(size_t)dev].ht.ensure((size_t)words * 4)) return EZ_EDEVICE;
-        a.ht_global = g_scratch[(size_t)dev].ht.as<uint32_t>();
+        Scratch &sc = g_scratch[std::make_pair(dev, hip_stream)];
+        if (sc.ht.ensure((size_t)words * 4)) return EZ_EDEVICE;
+        a.ht_global = sc.ht.as<uint32_t>();
     }
     if (write_idx) EZ_HIP(ez::launch_compress_split(a, a.ht_global, (hipStream_t)hip_stream));
     else EZ_HIP(ez::launch_compress(a, (hipStream_t)hip_stream));
