@@ -393,7 +393,7 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
 }  // namespace
 
 // two stream lists: K2g -> k2_fast hand-overs, k2_fast -> exact decoder hand-overs
-static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'f', 'g'
+static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'f', 'g', 'r', 'w'
 void select_decompress_variant(int v) { g_decompress_variant = v; }
 
 uint64_t decompress_workspace_words(uint64_t count) { return 2 * count + 32; }
@@ -405,11 +405,10 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
         return hipGetLastError();
     }
-    // long streams (slots of 64 KiB and more, C2/C4): a lane per stream moves 16 bytes per
-    // dependent step and few streams fill few lanes; the wave-per-stream decoder moves 64
+    // EZ_K2=exact (experiments): the exact decoder alone
     static const bool use_exact = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "exact") == 0;
     static const uint64_t long_slot = getenv("EZ_K2_LONG") ? (uint64_t)atoll(getenv("EZ_K2_LONG")) : (64u << 10);
-    if (use_exact || a.max_out >= long_slot) {
+    if (use_exact) {
         DecompressArgs b = a;
         b.slow = nullptr;
         uint64_t grid = b.count < (1u << 30) ? b.count : (1u << 30);
@@ -418,13 +417,22 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     }
     hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
+    if (g_decompress_variant < 0) {
+        const char *v = getenv("EZ_K2");
+        g_decompress_variant = v && strcmp(v, "group") == 0 ? 'g' : (v && strcmp(v, "fast") == 0 ? 'f' : (v && strcmp(v, "wave") == 0 ? 'w' : 0));
+    }
+    if (g_decompress_variant == 'w' || (g_decompress_variant == 0 && a.max_out >= long_slot)) {
+        // long streams (slots of 64 KiB and more, C2/C4): too few to give every lane one;
+        // K2w gives each a wave, and its hand-overs go to the exact decoder
+        e = launch_decompress_wave(a, st);
+        if (e != hipSuccess) return e;
+        const uint64_t grid = a.count < 4096 ? a.count : 4096;
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+        return hipGetLastError();
+    }
     // K2g (LDS group decoder) first when the slots are small; its hand-overs go
     // through k2_fast, whose hand-overs go to the exact decoder
     // K2g is opt-in: at C1 the lane-per-stream decoder is faster
-    if (g_decompress_variant < 0) {
-        const char *v = getenv("EZ_K2");
-        g_decompress_variant = v && strcmp(v, "group") == 0 ? 'g' : (v && strcmp(v, "fast") == 0 ? 'f' : 0);
-    }
     const uint32_t RG = g_decompress_variant == 'g' ? group_decode_region(a.max_out) : 0;
     if (RG) {
         uint32_t *list2 = a.slow + a.count + 16;

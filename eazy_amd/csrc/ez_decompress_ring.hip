@@ -26,6 +26,7 @@
 #include "ez_internal.h"
 #include "ez_wave.h"
 #include "ez_bytes.h"
+#include "ez_k2_parse.h"
 
 namespace ez {
 namespace {
@@ -38,6 +39,10 @@ constexpr int32_t kChunk = 128;          // output leaves the ring in whole 128-
 
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 
+// 16 bytes at y of the batch [lo, hi) (bytes from hi on read as 0)
+__host__ __device__ __forceinline__ V16 ld_in(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
+    return y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
+}
 __host__ __device__ __forceinline__ V16 ring_ld(const uint8_t *ring, int32_t p) {
     const uint8_t *q = ring + (p & (kRing - 1));
     return V16{*(const u64_ua *)q, *(const u64_ua *)(q + 8)};
@@ -65,6 +70,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     uint8_t *out = A.out + A.out_off[s];
     const int64_t cap64 = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
     const int64_t limit = A.block_size_limit;
+    const int32_t lim32 = limit == 0 || limit > 0x7fffffff ? 0x7fffffff : (int32_t)limit;  // 0: no limit
     // 32-bit positions; clamped loads need >= 16 input bytes in the batch and a 16-byte slot
     bool slow = in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16;
     const int32_t nb = slow ? 0 : (int32_t)nb64, cap = (int32_t)cap64;
@@ -74,7 +80,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     }
     int32_t i = 0, pos = 0, bsl = -1;  // bsl: log2 of the window after MetaReset (-1: none yet)
     V16 h{0, 0};                       // 16 bytes at b + i (the next header)
-    if (!slow) h = b + 16 <= in_end ? ld16v(b) : ld_clamped(b, A.in, in_end);
+    if (!slow) h = ld_in(b, A.in, in_end);
     // the token being written: rem bytes at dst from sp (input / HBM output) or from the ring
     int32_t rem = 0, dst = 0, step = 16, rp = 0, fl = 0;  // fl: output below it is in HBM
     const uint8_t *sp = b;
@@ -83,54 +89,24 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     for (;;) {
         if (rem == 0) {
             if (i >= nb) break;
-            const uint64_t lo = h.lo;
-            const uint32_t t0 = (uint32_t)lo & 0xff, l7 = t0 & 0x7f;
-            int32_t adv;
-            if (t0 == 0 || t0 == 0x80) {
-                if (t0 == 0) {  // padding (reader.go:221-224), a run of zero bytes at once
-                    adv = lo ? (int32_t)(__builtin_ctzll(lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
-                } else {
-                    // meta (continueMetaTag reader.go:272-325): header metas and breaks only
-                    const uint32_t mb = (uint32_t)(lo >> 8) & 0xff, mt = mb & 0xf8, ml = mb & 7;
-                    const int32_t mln = ml == 7 ? 0 : (1 << ml);
-                    const uint32_t marg = (uint32_t)(lo >> 16) & 0xff;
-                    const bool m_brk = mt == kMetaBreak && mln == 0;
-                    const bool m_rst = mt == kMetaReset && mln == 1 && marg <= 32 && pos == 0 && (limit == 0 || (1ll << marg) <= limit);
-                    const bool m_ver = mt == kMetaVer && mln == 1 && marg == 0;
-                    const bool m_mag = mt == kMetaMagic && mln == 4 && (uint32_t)(lo >> 16) == 0x797a6165u;
-                    if (ml == 6 || i + 2 + mln > nb || !(m_brk || m_rst || m_ver || m_mag)) { slow = true; break; }
-                    if (m_rst) bsl = (int32_t)marg;
-                    adv = 2 + mln;
-                }
-            } else {
-                // Decoder.Tag reader.go:346-392 and Decoder.Offset :394-420, by selects
-                const uint32_t lx = (uint32_t)(lo >> 8);
-                const int64_t L = l7 < 124 ? (int64_t)l7
-                                : (l7 == 124 ? 124 + (int64_t)(lx & 0xff) : (l7 == 125 ? 380 + (int64_t)(lx & 0xffff) : 65916 + (int64_t)lx));
-                const uint32_t j = l7 < 124 ? 1 : (l7 == 124 ? 2 : (l7 == 125 ? 3 : 5));
-                const bool cp = (t0 & 0x80) != 0;
-                const uint64_t x = fun8(lo, h.hi, j);  // bytes from the offset on (header <= 11 bytes)
-                const bool lng = (x & 0xff) == 0xff;
-                const uint64_t y = lng ? fun8(lo, h.hi, j + 1) : x;
-                const uint32_t o = (uint32_t)y & 0xff, ox = (uint32_t)(y >> 8);
-                const int64_t D0 = o < 252 ? (int64_t)o : (o == 252 ? 252 + (int64_t)(ox & 0xff) : (o == 253 ? 508 + (int64_t)(ox & 0xffff) : 66044 + (int64_t)ox));
-                const uint32_t k = o < 252 ? 1 : (o == 252 ? 2 : (o == 253 ? 3 : 5));
-                const int64_t D = lng ? D0 : D0 + L;
-                adv = cp ? (int32_t)(j + (lng ? 1 : 0) + k) : (int32_t)(j + L);
-                const int64_t bs = bsl < 0 ? 0 : (1ll << bsl);
-                const bool bad = l7 == 127 || (cp && o == 255) || (limit != 0 && L > limit) || bs == 0 ||
-                                 pos + L > cap || (int64_t)i + (cp ? (int64_t)adv : (int64_t)j + L) > nb || (cp && D > bs);
-                if (bad) { slow = true; break; }  // the exact decoder takes the stream
+            K2Tok t;
+            const int r = k2_parse(h, i, nb, pos, cap, lim32, limit, bsl, t);
+            if (r == kParseHandOver) { slow = true; break; }  // the exact decoder takes the stream
+            const int32_t adv = t.adv;
+            if (r == kParseToken) {
+                const int32_t L = t.L;
+                const uint32_t j = (uint32_t)t.j, D = t.D;
+                const bool cp = t.cp;
                 dst = pos;
-                rem = (int32_t)L;
-                pos += (int32_t)L;
+                rem = L;
+                pos += L;
                 from_in = !cp;
                 near = cp && D <= kNear;
                 rp = dst - (int32_t)D;
                 sp = cp ? out + rp : b + (i + (int32_t)j);
                 patt = cp && D < 16;
                 step = 16;
-                if (!cp && (int64_t)j + L <= 16) {  // a short literal is in the header's 16 bytes already
+                if (!cp && (int32_t)j + L <= 16) {  // a short literal is in the header's 16 bytes already
                     patt = true;
                     pv = shr16(h, j);
                 }
@@ -148,7 +124,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             }
             i += adv;
             // the next header, loaded beside this token's first move
-            if (i < nb) h = b + i + 16 <= in_end ? ld16v(b + i) : ld_clamped(b + i, A.in, in_end);
+            if (i < nb) h = ld_in(b + i, A.in, in_end);
         }
         if (rem > 0) {
             V16 v;

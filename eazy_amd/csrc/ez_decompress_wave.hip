@@ -1,0 +1,202 @@
+// ez_decompress_wave.hip — K2w: batch decompression of long streams, one wave
+// per stream, the parse uniform (scalar) and every token's bytes produced by
+// the 64 lanes, 16 bytes each, with the stream's input and recent output in LDS.
+//
+// Restates Reader.Read to EOF for NewReaderBytes (reader.go:116-216 read,
+// readTag :218-270, continueMetaTag :272-325, Decoder :346-514) for the common
+// case through k2_parse (ez_k2_parse.h), as K2r does; anything else hands the
+// stream to the exact decoder (ez_decompress.hip).
+//
+// Why.  With streams of 64 KiB and more (C2: 4,096 x 256 KiB) there are too few
+// streams to give every lane one (K2r), and the exact wave decoder pays a global
+// round trip for every header byte it parses and every byte it copies.  Here a
+// token costs one LDS read of its header (the input is staged 512 bytes at a
+// time, one chunk ahead of the parse, in a 1 KiB input ring), a scalar parse,
+// and one LDS read + write per 16 output bytes per lane: copies read the last
+// 8 KiB of output from an LDS ring, farther ones the output already in HBM.
+// Output leaves the ring 1 KiB at a time (64 lanes x 16 bytes, whole lines).
+#include "ez_format.h"
+#include "ez_internal.h"
+#include "ez_wave.h"
+#include "ez_bytes.h"
+#include "ez_k2_parse.h"
+
+namespace ez {
+namespace {
+
+constexpr int32_t kWR = 8192;      // output ring bytes per stream (power of two)
+constexpr int32_t kWIn = 1024;     // input ring bytes per stream (power of two)
+constexpr int32_t kWStage = 512;   // input staged this many bytes at a time (32 lanes x 16)
+constexpr int32_t kWChunk = 1024;  // output leaves the ring this many bytes at a time
+constexpr size_t kWLds = 16 + (size_t)kWR + 32 + kWIn + 16;
+
+typedef uint64_t __attribute__((aligned(1))) u64_ua;
+
+template <int32_t R>
+__device__ __forceinline__ V16 rld(const uint8_t *ring, int32_t p) {
+    const uint8_t *q = ring + (p & (R - 1));
+    return V16{*(const u64_ua *)q, *(const u64_ua *)(q + 8)};
+}
+// 16 bytes of position p into a ring of R bytes laid out as [16-byte guard][R bytes]
+// [16-byte mirror of the first 16][16-byte guard]: a write that wraps is written again
+// R bytes lower (its head lands in the front guard), one into the first 16 bytes again
+// R bytes higher (its tail lands in the back guard) -- whole 16-byte LDS writes only
+template <int32_t R>
+__device__ __forceinline__ void rst(uint8_t *ring, int32_t p, V16 v) {
+    const int32_t r = p & (R - 1);
+    *(u64_ua *)(ring + r) = v.lo;
+    *(u64_ua *)(ring + r + 8) = v.hi;
+    if (r > R - 16 || r < 16) {
+        const int32_t r2 = r < 16 ? r + R : r - R;
+        *(u64_ua *)(ring + r2) = v.lo;
+        *(u64_ua *)(ring + r2 + 8) = v.hi;
+    }
+}
+
+__device__ __forceinline__ V16 ld_in(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
+    return y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
+}
+
+// stream s by the whole wave; false = hand it over
+__device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring, uint8_t *inb, const int lane) {
+    const uint8_t *b = A.in + A.in_off[s];
+    const int64_t nb64 = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
+    const uint8_t *in_end = A.in + A.in_off[A.count];
+    uint8_t *out = A.out + A.out_off[s];
+    const int64_t cap64 = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    const int64_t limit = A.block_size_limit;
+    const int32_t lim32 = limit == 0 || limit > 0x7fffffff ? 0x7fffffff : (int32_t)limit;
+    if (in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16) return false;
+    const int32_t nb = (int32_t)nb64, cap = (int32_t)cap64;
+    // zero ring = the fresh window's zero history
+    for (int32_t k = 16 * lane - 16; k < kWR + 32; k += 1024) {
+        *(u64_ua *)(ring + k) = 0;
+        *(u64_ua *)(ring + k + 8) = 0;
+    }
+    // input ring: bytes [in_hi - kWIn, in_hi) staged; pend = the next chunk, in flight
+    auto put_in = [&](int32_t x, V16 v) {
+        if (lane < kWStage / 16) {
+            const int32_t r = (x + 16 * lane) & (kWIn - 1);
+            *(u64_ua *)(inb + r) = v.lo;
+            *(u64_ua *)(inb + r + 8) = v.hi;
+            if (r == 0) {
+                *(u64_ua *)(inb + kWIn) = v.lo;
+                *(u64_ua *)(inb + kWIn + 8) = v.hi;
+            }
+        }
+    };
+    auto get_in = [&](int32_t x) { return lane < kWStage / 16 ? ld_in(b + x + 16 * lane, A.in, in_end) : V16{0, 0}; };
+    int32_t in_hi = 0;
+    for (; in_hi < kWIn; in_hi += kWStage) put_in(in_hi, get_in(in_hi));
+    V16 pend = get_in(in_hi);
+
+    int32_t i = 0, pos = 0, bsl = -1, fl = 0;  // fl: output below it is in HBM
+    while (i < nb) {
+        if (i + 96 > in_hi) {  // the scan below reads input bytes i .. i+79
+            if (i + 96 > in_hi + kWStage) {  // past a long literal: stage afresh
+                in_hi = i & ~(kWStage - 1);
+                for (int32_t e = in_hi + kWIn; in_hi < e; in_hi += kWStage) put_in(in_hi, get_in(in_hi));
+            } else {
+                put_in(in_hi, pend);
+                in_hi += kWStage;
+            }
+            pend = get_in(in_hi);
+        }
+        // every lane scans the step that would start at input byte i + lane; the steps
+        // then run in order from i, each reading its scan from its start's lane
+        uint32_t w0, w1, w2;
+        {
+            K2Tok c;
+            const int rs = k2_scan(rld<kWIn>(inb, i + lane), i + lane, nb, lim32, limit, c);
+            const uint32_t adv_small = rs == kParseToken && !c.cp ? 0u : (uint32_t)c.adv;  // <= 34 unless a literal
+            w0 = (uint32_t)c.L;
+            w1 = c.D;
+            w2 = (uint32_t)(rs + 1) | ((uint32_t)c.cp << 2) | ((uint32_t)c.j << 3) | (adv_small << 6) | (c.marg << 16);
+        }
+        int32_t p = 0;
+        while (p < 64 && i + p < nb) {
+            const uint32_t x2 = (uint32_t)__builtin_amdgcn_readlane((int)w2, p);
+            K2Tok t;
+            t.cp = (x2 >> 2) & 1;
+            t.j = (int32_t)((x2 >> 3) & 7);
+            t.marg = (x2 >> 16) & 63;
+            t.L = __builtin_amdgcn_readlane((int)w0, p);
+            t.D = (uint32_t)__builtin_amdgcn_readlane((int)w1, p);
+            int r = (int)(x2 & 3) - 1;
+            t.adv = r == kParseToken && !t.cp ? t.j + t.L : (int32_t)((x2 >> 6) & 1023);
+            r = k2_check(r, t, pos, cap, bsl);
+            if (r == kParseHandOver) return false;
+            if (r == kParseToken) {
+                const int32_t L = t.L;
+                const int32_t D = (int32_t)t.D;
+                // lane's bytes of the token: [q, q + 16) for q = done + lane * step
+                int32_t step = 16, W = 16 * 64;
+                V16 pv{0, 0};
+                if (t.cp && D < 16) {
+                    if (D > 0) {  // a short-period run: its 16-byte pattern every `step` bytes
+                        const uint32_t per = (uint32_t)D;
+                        pv = run_pattern(shr16(rld<kWR>(ring, pos - 16), 16 - per), per);
+                        step = (int32_t)(per * (16 / per));
+                    }
+                    W = 64 * step;
+                } else if (t.cp) {
+                    W = D & ~15;  // reads stay below the bytes this pass writes
+                    W = W < 1024 ? W : 1024;
+                }
+                const int32_t src = i + p + t.j;                        // literal
+                const bool staged = !t.cp && src + L <= in_hi;         // its bytes in the input ring
+                for (int32_t done = 0; done < L; done += W) {
+                    const int32_t q = done + step * lane;
+                    const bool act = step * lane < W && q < L;
+                    // ring slots of positions >= rlo are intact; below it the output is in HBM
+                    const int32_t sq = pos + q - D, rlo = pos + done + 16 - kWR;
+                    if (act) {
+                        V16 v = pv;
+                        if (!t.cp) v = staged ? rld<kWIn>(inb, src + q) : ld_in(b + src + q, A.in, in_end);
+                        else if (D >= 16) v = sq >= rlo ? rld<kWR>(ring, sq) : (sq >= 0 ? ld16v(out + sq) : ld_clamped(out + sq, out, out + cap));
+                        rst<kWR>(ring, pos + q, v);
+                    }
+                    const int32_t fin = pos + (done + W < L ? done + W : L);  // final bytes end here
+                    while (fin >= fl + kWChunk) {
+                        st16v(out + fl + 16 * lane, rld<kWR>(ring, fl + 16 * lane));
+                        fl += kWChunk;
+                    }
+                }
+                pos += L;
+            }
+            p += t.adv;
+        }
+        i += p;
+    }
+    for (int32_t q = fl + 16 * lane; q < pos; q += 1024) {  // the last partial chunk, exact bytes
+        const V16 v = rld<kWR>(ring, q);
+        if (q + 16 <= pos) st16v(out + q, v);
+        else put_small(out + q, v, (uint32_t)(pos - q));
+    }
+    if (lane == 0) {
+        A.out_size[s] = (uint64_t)pos;
+        if (A.status) A.status[s] = EZ_OK;
+    }
+    return true;
+}
+
+__global__ __launch_bounds__(64) void k2_wave(DecompressArgs A) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint8_t *ring = smem + 16, *inb = smem + 16 + kWR + 32;
+    const int lane = (int)threadIdx.x;
+    for (uint64_t s = blockIdx.x; s < A.count; s += gridDim.x)
+        if (!wave_one(A, s, ring, inb, lane) && lane == 0) {
+            const uint32_t at = atomicAdd(&A.slow[0], 1u);
+            A.slow[1 + at] = (uint32_t)s;
+        }
+}
+
+}  // namespace
+
+hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t st) {
+    const uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);
+    hipLaunchKernelGGL(k2_wave, dim3((unsigned)grid), dim3(64), kWLds, st, a);
+    return hipGetLastError();
+}
+
+}  // namespace ez

@@ -106,7 +106,8 @@ uint32_t group_decode_region(uint64_t max_out);
 hipError_t launch_decompress_group(const DecompressArgs &a, uint32_t R, hipStream_t s);
 void select_decompress_variant(int v);
 // K2r: one lane per stream with a 512-byte LDS ring of recent output (ez_decompress_ring.hip)
-hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t s);  // 0 = automatic, 'f' fast, 'g' group (tests, A/B)
+hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t s);
+hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t s);  // K2w, long streams  // 0 = automatic, 'f' fast, 'g' group (tests, A/B)
 hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
                        uint8_t *packed, uint64_t *packed_off, void *workspace, hipStream_t s);
 size_t pack_workspace(uint64_t count);

@@ -1,0 +1,113 @@
+// ez_k2_parse.h — the token parse shared by the batch decoders K2r (lane per
+// stream) and K2w (wave per stream): one step of Reader.read's readTag for the
+// common case, from the 16 input bytes at the parse position.
+//
+// readTag reader.go:218-270 (padding :221-224), continueMetaTag :272-325 for
+// the header metas (magic, version 0, MetaReset before any output) and breaks,
+// Decoder.Tag :346-392 and Decoder.Offset :394-420.  Everything else — an
+// error of any kind, an unsupported or wide meta, a reset after output, a
+// length over BlockSizeLimit, a token past the output slot or the input, a
+// 4-byte length or offset of 2^30 or more — is "hand over": the exact decoder
+// (ez_decompress.hip) recomputes the stream from scratch.
+#pragma once
+
+#include "ez_bytes.h"
+#include "ez_format.h"
+
+namespace ez {
+
+struct K2Tok {
+    int32_t adv;    // input bytes the step consumes
+    int32_t L;      // token length (0: padding or a meta)
+    int32_t j;      // literal: its bytes start at i + j
+    uint32_t D;     // copy distance (0: zero region)
+    bool cp;        // copy (else literal)
+    uint32_t marg;  // kScanReset: log2 of the window
+};
+
+enum { kParseSkip = 0, kParseToken = 1, kParseHandOver = -1 };
+enum { kScanReset = 2 };  // k2_scan only: a MetaReset, valid only before any output
+
+// The checks that do not depend on the decoder's state, for a step at input position
+// i: returns kParseSkip (padding, break, version, magic), kScanReset, kParseToken or
+// kParseHandOver.  h = input bytes i .. i+15 (zeros past the batch); nb = stream
+// bytes; lim32 = BlockSizeLimit clamped to 32 bits (0x7fffffff: none), limit = the 64-bit one
+__host__ __device__ __forceinline__ int k2_scan(V16 h, int32_t i, int32_t nb, int32_t lim32, int64_t limit, K2Tok &t) {
+    const uint64_t lo = h.lo;
+    const uint32_t t0 = (uint32_t)lo & 0xff, l7 = t0 & 0x7f;
+    t.L = 0;
+    t.j = 0;
+    t.D = 0;
+    t.cp = false;
+    t.marg = 0;
+    if (t0 == 0) {  // padding, a run of zero bytes at once
+        t.adv = lo ? (int32_t)(__builtin_ctzll(lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
+        return kParseSkip;
+    }
+    if (t0 == 0x80) {
+        // meta: header metas and breaks only
+        const uint32_t mb = (uint32_t)(lo >> 8) & 0xff, mt = mb & 0xf8, ml = mb & 7;
+        const int32_t mln = ml == 7 ? 0 : (1 << ml);
+        const uint32_t marg = (uint32_t)(lo >> 16) & 0xff;
+        const bool m_brk = mt == kMetaBreak && mln == 0;
+        const bool m_rst = mt == kMetaReset && mln == 1 && marg <= 32 && (limit == 0 || (1ll << marg) <= limit);
+        const bool m_ver = mt == kMetaVer && mln == 1 && marg == 0;
+        const bool m_mag = mt == kMetaMagic && mln == 4 && (uint32_t)(lo >> 16) == 0x797a6165u;
+        if (ml == 6 || i + 2 + mln > nb || !(m_brk || m_rst || m_ver || m_mag)) return kParseHandOver;
+        t.adv = 2 + mln;
+        t.marg = marg;
+        return m_rst ? kScanReset : kParseSkip;
+    }
+    // Tag and Offset in 32 bits, branch-free: a length byte l7 >= 124 is followed by
+    // 1 << (l7 - 124) little-endian bytes over the base 124 / 380 / 65916, an offset
+    // byte o >= 252 by 1 << (o - 252) bytes over 252 / 508 / 66044
+    const uint32_t lx = (uint32_t)(lo >> 8);
+    const bool lw = l7 >= 124;
+    const uint32_t ln = lw ? 1u << (l7 - 124 < 2 ? l7 - 124 : 2) : 0u;  // extra length bytes (1, 2, 4; 127 is bad)
+    const uint32_t lmask = ln == 4 ? 0x3fffffffu : (1u << (8 * ln)) - 1;  // (4 bytes >= 2^30 are bad)
+    const int32_t L = lw ? 124 + (l7 >= 125 ? 256 : 0) + (l7 >= 126 ? 65536 : 0) + (int32_t)(lx & lmask) : (int32_t)l7;
+    const uint32_t j = 1 + ln;
+    const bool cp = (t0 & 0x80) != 0;
+    const bool lng = ((uint32_t)(lo >> (8 * j)) & 0xff) == 0xff;  // byte j (j <= 5, in lo)
+    const uint32_t jo = j + (lng ? 1 : 0);
+    const uint64_t y = (lo >> (8 * jo)) | (h.hi << (64 - 8 * jo));  // bytes from the offset on (1 <= jo <= 6)
+    const uint32_t o = (uint32_t)y & 0xff, ox = (uint32_t)(y >> 8);
+    const bool ow = o >= 252;
+    const uint32_t on = ow ? 1u << (o - 252 < 2 ? o - 252 : 2) : 0u;
+    const uint32_t omask = on == 4 ? 0x3fffffffu : (1u << (8 * on)) - 1;
+    const int32_t D0 = ow ? 252 + (o >= 253 ? 256 : 0) + (o >= 254 ? 65536 : 0) + (int32_t)(ox & omask) : (int32_t)o;
+    const uint32_t k = 1 + on;
+    const uint32_t D = lng ? (uint32_t)D0 : (uint32_t)D0 + (uint32_t)L;  // < 2^32
+    const int32_t adv = cp ? (int32_t)(jo + k) : (int32_t)j + L;
+    const bool bad = l7 == 127 || (l7 == 126 && lx >= (1u << 30)) || (cp && o >= 254 && (o == 255 || ox >= (1u << 30))) || L > lim32 ||
+                     (uint32_t)i + (uint32_t)adv > (uint32_t)nb || (cp && D >= (1u << 30));
+    if (bad) return kParseHandOver;
+    t.adv = adv;
+    t.L = L;
+    t.j = (int32_t)j;
+    t.D = cp ? D : 0;
+    t.cp = cp;
+    return kParseToken;
+}
+
+// the checks on the decoder's state: output position pos in a slot of cap bytes and
+// bsl = log2 of the window after MetaReset (-1: none yet; updated here)
+__host__ __device__ __forceinline__ int k2_check(int r, const K2Tok &t, int32_t pos, int32_t cap, int32_t &bsl) {
+    if (r == kScanReset) {
+        if (pos != 0) return kParseHandOver;
+        bsl = (int32_t)t.marg;
+        return kParseSkip;
+    }
+    if (r == kParseToken &&
+        (bsl < 0 || (uint32_t)pos + (uint32_t)t.L > (uint32_t)cap || (t.cp && bsl < 30 && t.D > (1u << bsl))))
+        return kParseHandOver;
+    return r;
+}
+
+// one step at input position i with the decoder at output position pos
+__host__ __device__ __forceinline__ int k2_parse(V16 h, int32_t i, int32_t nb, int32_t pos, int32_t cap, int32_t lim32, int64_t limit,
+                                                 int32_t &bsl, K2Tok &t) {
+    return k2_check(k2_scan(h, i, nb, lim32, limit, t), t, pos, cap, bsl);
+}
+
+}  // namespace ez

@@ -8,7 +8,7 @@ rocprofv3 -L > $R/gpurun_out/pmc/counters.txt 2>&1 || true
 i=0
 for C in "${@}"; do
   i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $R/gpurun_out/pmc/p$i -o run -- python3 bench.py --no-cpu --steps 2 --warmup 1 > $R/gpurun_out/pmc/p$i.log 2>&1
+  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $R/gpurun_out/pmc/p$i -o run -- python3 bench.py --no-cpu --steps 2 --warmup 1 ${BENCH_ARGS:-} > $R/gpurun_out/pmc/p$i.log 2>&1
   rc=$?
   echo "pass $i rc=$rc: $C"
   [ $rc -ne 0 ] && tail -5 $R/gpurun_out/pmc/p$i.log && exit $rc

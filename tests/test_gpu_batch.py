@@ -42,14 +42,14 @@ def _run(cuda, bufs, block=MiB, htable=1024, magic=True):
     out2, sizes2, status2 = ez.decompress_batch(packed, poff, off, exact_only=True)
     mx = int(lens.max()) if len(lens) else 0
     others = [ez.decompress_batch(packed, poff, off, max_len=mx)]
-    for kind in ("f", "g"):
+    for kind in ("f", "g", "w"):
         ez.select_decompress_kernel(kind)
         try:
             others.append(ez.decompress_batch(packed, poff, off, max_len=mx))
         finally:
             ez.select_decompress_kernel("")
     torch.cuda.synchronize()
-    # the ring decoder (default), the lane-per-stream decoder, the LDS group decoder and the exact decoder agree
+    # the ring decoder (default), the lane-per-stream, LDS group and wave-per-stream decoders and the exact decoder agree
     assert torch.equal(status, status2) and torch.equal(sizes, sizes2)
     assert torch.equal(out[: int(offs[-1])], out2[: int(offs[-1])])
     for o, z, st in others:

@@ -166,7 +166,8 @@ def test_batch_decoders_on_damaged_streams(cuda):
     coff = torch.from_numpy(offs).to(cuda)
     for cap in (4096, 8192):
         ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-        for kind, kw in (("", {"max_len": cap}), ("f", {"max_len": cap}), ("g", {"max_len": cap}), ("", {}), ("", {"exact_only": True})):
+        for kind, kw in (("", {"max_len": cap}), ("f", {"max_len": cap}), ("g", {"max_len": cap}), ("w", {"max_len": cap}), ("", {}),
+                         ("", {"exact_only": True})):
             ez.select_decompress_kernel(kind)
             try:
                 out, sizes, status = ez.decompress_batch(comp, coff, ooff, **kw)

@@ -19,7 +19,8 @@ EMU = os.path.join(ROOT, "tools", "ring_emu")
 @pytest.fixture(scope="module")
 def emu():
     src = os.path.join(ROOT, "tools", "ring_emu.hip")
-    deps = [src] + [os.path.join(ROOT, "eazy_amd", "csrc", f) for f in ("ez_decompress_ring.hip", "ez_bytes.h", "ez_format.h", "ez_internal.h")]
+    deps = [src] + [os.path.join(ROOT, "eazy_amd", "csrc", f) for f in ("ez_decompress_ring.hip", "ez_k2_parse.h", "ez_bytes.h", "ez_format.h",
+                                                                              "ez_internal.h")]
     if not os.path.exists(EMU) or os.path.getmtime(EMU) < max(os.path.getmtime(d) for d in deps):
         p = subprocess.run(["/opt/rocm/bin/hipcc", "-O1", "-std=c++17", "--offload-arch=gfx950", "-Wno-align-mismatch",
                             "-o", EMU, src], capture_output=True, text=True, timeout=600)
