@@ -53,6 +53,23 @@ __device__ __forceinline__ void rst(uint8_t *ring, int32_t p, V16 v) {
     }
 }
 
+// the first n bytes (1..16) of v at d, and rput: n bytes of position p into the ring
+// (exact, so pieces of one instruction never overlap)
+__device__ __forceinline__ void put_n(uint8_t *d, V16 v, uint32_t n) {
+    if (n >= 16) {
+        *(u64_ua *)d = v.lo;
+        *(u64_ua *)(d + 8) = v.hi;
+    } else {
+        put_small(d, v, n);
+    }
+}
+template <int32_t R>
+__device__ __forceinline__ void rput(uint8_t *ring, int32_t p, V16 v, uint32_t n) {
+    const int32_t r = p & (R - 1);
+    put_n(ring + r, v, n);
+    if (r + (int32_t)n > R || r < 16) put_n(ring + (r < 16 ? r + R : r - R), v, n);
+}
+
 __device__ __forceinline__ V16 ld_in(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
     return y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
 }
@@ -91,6 +108,28 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
     V16 pend = get_in(in_hi);
 
     int32_t i = 0, pos = 0, bsl = -1, fl = 0;  // fl: output below it is in HBM
+    // A group: tokens whose sources lie before the group's first output byte gpos
+    // (literals staged in the input ring, copies with D >= L from the output ring),
+    // cut into pieces of <= 16 bytes, one per lane: one LDS read and one exact write
+    // for all of them.  Lane l's piece: gn bytes to output position gd from gs (input
+    // ring if gi, else output ring).
+    int32_t used = 0, gpos = 0, gd = 0, gs = 0;
+    uint32_t gn = 0;
+    bool gi = false;
+    auto run_group = [&]() {
+        if (used > 0) {
+            if (lane < used) {
+                const uint8_t *a = gi ? inb + (gs & (kWIn - 1)) : ring + (gs & (kWR - 1));
+                rput<kWR>(ring, gd, V16{*(const u64_ua *)a, *(const u64_ua *)(a + 8)}, gn);
+            }
+            while (pos >= fl + kWChunk) {
+                st16v(out + fl + 16 * lane, rld<kWR>(ring, fl + 16 * lane));
+                fl += kWChunk;
+            }
+            used = 0;
+        }
+        gpos = pos;
+    };
     while (i < nb) {
         if (i + 96 > in_hi) {  // the scan below reads input bytes i .. i+79
             if (i + 96 > in_hi + kWStage) {  // past a long literal: stage afresh
@@ -104,10 +143,61 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
         }
         // every lane scans the step that would start at input byte i + lane; the steps
         // then run in order from i, each reading its scan from its start's lane
+        K2Tok c;
+        c.adv = 1;
+        const int rs = k2_scan(rld<kWIn>(inb, i + lane), i + lane, nb, lim32, limit, c);
+        // Fast path: the steps from i (walked on the scalar unit: M = their starts) are
+        // tokens, paddings and header metas, and no copy reads output of this batch.  Then
+        // every token is produced by its start's lane at once, 16 bytes per round.
+        {
+            const int32_t advl = rs == kParseHandOver ? 64 : c.adv;
+            uint64_t M = 0;
+            int32_t pe = 0;
+            while (pe < 64 && i + pe < nb) {
+                M |= 1ull << pe;
+                pe += __builtin_amdgcn_readlane(advl, pe);
+            }
+            const bool st = (M >> lane) & 1;
+            const bool tok = st && rs == kParseToken;
+            const int32_t Ll = tok ? c.L : 0;
+            int32_t incl = Ll;
+#pragma unroll
+            for (int d = 1; d < 64; d <<= 1) {
+                const int32_t v = __shfl_up(incl, d, 64);
+                if (lane >= d) incl += v;
+            }
+            const int32_t total = __builtin_amdgcn_readlane(incl, 63);
+            const int32_t dst = pos + incl - Ll;
+            const int32_t cs = dst - (int32_t)c.D;  // a copy's source
+            bool ok = !(st && (rs == kParseHandOver || rs == kScanReset));
+            if (tok) {
+                ok = ok && c.L <= 256 && bsl >= 0;
+                // the source: before this batch's output, and in ring slots none of its writes reach
+                if (c.cp) ok = ok && (c.D == 0 || (cs + c.L <= pos && cs >= pos + total + 16 - kWR)) && (bsl >= 30 || c.D <= (1u << bsl));
+                else ok = ok && i + lane + c.j + c.L <= in_hi;
+            }
+            if (__ballot(!ok) == 0 && (uint32_t)pos + (uint32_t)total <= (uint32_t)cap) {
+                for (int32_t k = 0; __ballot(tok && 16 * k < c.L) != 0; k++) {
+                    if (tok && 16 * k < c.L) {
+                        V16 v{0, 0};  // a zero region's
+                        if (!c.cp) v = rld<kWIn>(inb, i + lane + c.j + 16 * k);
+                        else if (c.D != 0) v = rld<kWR>(ring, cs + 16 * k);
+                        rput<kWR>(ring, dst + 16 * k, v, (uint32_t)(c.L - 16 * k < 16 ? c.L - 16 * k : 16));
+                    }
+                }
+                pos += total;
+                i += pe;
+                while (pos >= fl + kWChunk) {
+                    st16v(out + fl + 16 * lane, rld<kWR>(ring, fl + 16 * lane));
+                    fl += kWChunk;
+                }
+                gpos = pos;
+                continue;
+            }
+        }
+        // otherwise step by step
         uint32_t w0, w1, w2;
         {
-            K2Tok c;
-            const int rs = k2_scan(rld<kWIn>(inb, i + lane), i + lane, nb, lim32, limit, c);
             const uint32_t adv_small = rs == kParseToken && !c.cp ? 0u : (uint32_t)c.adv;  // <= 34 unless a literal
             w0 = (uint32_t)c.L;
             w1 = c.D;
@@ -126,8 +216,25 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
             t.adv = r == kParseToken && !t.cp ? t.j + t.L : (int32_t)((x2 >> 6) & 1023);
             r = k2_check(r, t, pos, cap, bsl);
             if (r == kParseHandOver) return false;
-            if (r == kParseToken) {
-                const int32_t L = t.L;
+            const int32_t L = t.L, np = (L + 15) >> 4;
+            const int32_t src = i + p + t.j;  // literal
+            // a piece of a group: a literal whose bytes are staged, a copy with D >= L whose
+            // source is still in the ring
+            const bool piece = r == kParseToken && np <= 64 &&
+                               (t.cp ? (t.D >= (uint32_t)L && pos - (int32_t)t.D >= pos + 16 - kWR) : src + L <= in_hi);
+            if (piece) {
+                if (used + np > 64 || (t.cp && pos - (int32_t)t.D + L > gpos)) run_group();
+                const uint32_t k = (uint32_t)(lane - used);
+                if (k < (uint32_t)np) {
+                    gd = pos + 16 * (int32_t)k;
+                    gs = (t.cp ? pos - (int32_t)t.D : src) + 16 * (int32_t)k;
+                    gi = !t.cp;
+                    gn = (uint32_t)(L - 16 * (int32_t)k < 16 ? L - 16 * (int32_t)k : 16);
+                }
+                used += np;
+                pos += L;
+            } else if (r == kParseToken) {
+                run_group();
                 const int32_t D = (int32_t)t.D;
                 // lane's bytes of the token: [q, q + 16) for q = done + lane * step
                 int32_t step = 16, W = 16 * 64;
@@ -143,7 +250,6 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
                     W = D & ~15;  // reads stay below the bytes this pass writes
                     W = W < 1024 ? W : 1024;
                 }
-                const int32_t src = i + p + t.j;                        // literal
                 const bool staged = !t.cp && src + L <= in_hi;         // its bytes in the input ring
                 for (int32_t done = 0; done < L; done += W) {
                     const int32_t q = done + step * lane;
@@ -163,9 +269,11 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
                     }
                 }
                 pos += L;
+                gpos = pos;
             }
             p += t.adv;
         }
+        run_group();  // before the input ring moves on
         i += p;
     }
     for (int32_t q = fl + 16 * lane; q < pos; q += 1024) {  // the last partial chunk, exact bytes

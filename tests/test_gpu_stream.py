@@ -177,6 +177,62 @@ def test_batch_decoders_on_damaged_streams(cuda):
             _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
 
 
+def _tag(t, n):
+    """Encoder.Tag (writer.go:537-563) for lengths < 65916."""
+    if n < 124:
+        return bytes([t | n])
+    if n < 380:
+        return bytes([t | 0x7C, n - 124])
+    return bytes([t | 0x7D]) + (n - 380).to_bytes(2, "little")
+
+
+def _off(d, n):
+    """Encoder.Offset (writer.go:565-597) for d >= n, d - n < 66044."""
+    o = d - n
+    if o < 252:
+        return bytes([o])
+    if o < 508:
+        return bytes([0xFC, o - 252])
+    return bytes([0xFD]) + (o - 508).to_bytes(2, "little")
+
+
+def test_batch_decoders_ring_edge_distances(cuda):
+    """Hand-built streams of short copies from 7.9-8.2 KiB back with short literals
+    between them: next to the wave decoder's 8 KiB output ring (K2w), whose steps
+    write ring slots close to the ones they read.  Every decoder gives the oracle's bytes."""
+    import torch
+
+    import eazy_amd as ez
+
+    rng = np.random.default_rng(5)
+    ins = []
+    for lo, hi in ((7800, 8000), (8000, 8150), (8100, 8200), (8150, 8190), (8170, 8300), (100, 9000)):
+        first = rng.integers(0, 256, 8400, dtype=np.uint8).tobytes()
+        c = bytearray(b"\x80\x02eazy\x80\x10\x14" + _tag(0x00, len(first)) + first)
+        n = len(first)
+        while n < 70000:
+            L = int(rng.integers(6, 40))
+            c += _tag(0x80, L) + _off(int(rng.integers(lo, hi)), L)
+            n += L
+            k = int(rng.integers(1, 6))
+            c += _tag(0x00, k) + rng.integers(0, 256, k, dtype=np.uint8).tobytes()
+            n += k
+        ins.append(bytes(c))
+    offs = np.concatenate([[0], np.cumsum([len(b) for b in ins])]).astype(np.int64)
+    comp = torch.from_numpy(np.frombuffer(b"".join(ins), np.uint8).copy()).to(cuda)
+    coff = torch.from_numpy(offs).to(cuda)
+    cap = 72 << 10
+    ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
+    for kind in ("", "w", "r"):
+        ez.select_decompress_kernel(kind)
+        try:
+            out, sizes, status = ez.decompress_batch(comp, coff, ooff, max_len=cap)
+            torch.cuda.synchronize()
+        finally:
+            ez.select_decompress_kernel("")
+        _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
+
+
 def _cmp_oracle(ins, cap, out, sizes, status):
     import eazy_amd as ez
     import oracle as orc
