@@ -146,8 +146,8 @@ def select_compress_kernel(kind: str = "") -> None:
 
 
 def select_decompress_kernel(kind: str = "") -> None:
-    """Force the first K2 kernel of later batch decodes ('f', 'g'; '' =
-    automatic).  Tests and A/B measurement only."""
+    """Force the first K2 kernel of later batch decodes ('r', 'f', 'g', 'w';
+    '' = automatic).  Tests and A/B measurement only."""
     _check(_lib().ez_select_decompress_kernel(ord(kind) if kind else 0))
 
 

@@ -180,7 +180,9 @@ int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t
 int ez_select_compress_kernel(int kind);
 /* Testing / A-B measurement: the first K2 kernel of later batch decodes with a
  * workspace ('r' lane-per-stream with an LDS ring of recent output, 'f'
- * lane-per-stream, 'g' LDS group decoder (needs a max_len hint); 0 = automatic).  Streams either cannot take go on to the exact decoder. */
+ * lane-per-stream, 'g' LDS group decoder (needs a max_len hint), 'w' wave per
+ * stream with LDS input and output rings; 0 = automatic: 'w' for slots of 64 KiB
+ * and more, else 'r').  Streams either cannot take go on to the exact decoder. */
 int ez_select_decompress_kernel(int kind);
 
 #ifdef __cplusplus
