@@ -564,3 +564,7 @@ def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=Non
     ws = None if exact_only else workspace.data_ptr()
     _check(_lib().ez_decompress_batch(block_size_limit, C.byref(b), ws, _stream_ptr(stream)))
     return out, sizes, status
+
+
+# ---------------------------------------------------------------- Dumper (reader.go:43-54, 545-768)
+from .dump import Dump, Dumper, NewDumper  # noqa: E402,F401
