@@ -49,7 +49,9 @@ enum Kind : int { kReject = 0, kWin = 1, kRun = 2, kCut = 3, kZero = 4 };
 // Stream input view: LDS-staged (PL) or global.
 template <bool PL>
 struct InView {
+    static constexpr bool kLds = PL;
     const uint8_t *g;      // global bytes of the stream
+    const uint8_t *lo, *hi;  // the batch's input bytes (16-byte loads stay inside)
     const uint32_t *gw;    // global aligned words covering g
     uint64_t gr;           // g - gw (bytes)
     uint64_t glast;        // last valid word index of gw
@@ -89,7 +91,18 @@ __device__ __forceinline__ void put_bytes(OutBuf &o, const V &P, int64_t src, in
     if (o.err) return;
     if (o.op + L > o.cap) { o.err = EZ_ENOSPC; return; }
     uint8_t *d = o.p + o.op;
-    for (int64_t k = lane; k < L; k += kWave) d[k] = (uint8_t)P.b(src + k);
+    if (!V::kLds && L >= 64) {
+        // global input: 16 bytes per lane, 1 KiB per wave step (a fresh stream's
+        // trailing literal is the whole Write when nothing matches, C4)
+        const uint8_t *q = P.g + src;
+        for (int64_t k = 16 * lane; k < L; k += 16 * kWave) {
+            const V16 v = q + k + 16 <= P.hi ? ld16v(q + k) : ld_clamped(q + k, P.lo, P.hi);
+            if (k + 16 <= L) st16v(d + k, v);
+            else put_small(d + k, v, (uint32_t)(L - k));
+        }
+    } else {
+        for (int64_t k = lane; k < L; k += kWave) d[k] = (uint8_t)P.b(src + k);
+    }
     o.op += L;
 }
 
@@ -136,6 +149,8 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     // ---- input view (+ LDS staging)
     InView<PL> P;
     P.g = A.in + ib;
+    P.lo = A.in;
+    P.hi = A.in + A.in_off[A.count];
     P.gr = (uint64_t)(uintptr_t)P.g & 3;
     P.gw = (const uint32_t *)(P.g - P.gr);
     P.glast = (P.gr + (uint64_t)n + 3) / 4;
