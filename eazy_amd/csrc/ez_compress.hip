@@ -216,6 +216,15 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     int64_t done = 0, i = 0;
     int64_t guard = 0;
     const int64_t guard_max = 16 * n + 4096;
+    // global input: the 16 bytes x-8 .. x+7 around each lane's position, and those of
+    // the window after this one if nothing is accepted (loaded while this one is judged)
+    const bool pf = !PL && in_hi - in_lo >= 16;
+    auto around = [&](int64_t y) -> V16 {
+        const uint8_t *q = P.g + y - 8;
+        return q >= in_lo && q + 16 <= in_hi ? ld16v(q) : ld_clamped(q, in_lo, in_hi);
+    };
+    V16 nxt_w{0, 0};
+    int64_t nxt_i = -1;
 
     while (i + 4 <= n && !o.err) {
         if (++guard > guard_max) { o.err = EZ_ESTUCK; break; }
@@ -224,10 +233,16 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         const int nvalid = rem < kWave ? (int)rem : kWave;
         const int64_t x = i + lane;
         const bool valid = lane < nvalid;
+        V16 cur{0, 0};  // bytes x-8 .. x+7 (pf)
+        if (pf) {
+            cur = nxt_i == i ? nxt_w : around(x);
+            nxt_w = around(x + nvalid);
+            nxt_i = i + nvalid;
+        }
 
         // -- hash + intra-window predecessor / successor with the same hash
         uint32_t h = 0xffffffffu;
-        if (valid) h = (P.u32(x) * kHashMul) >> hsh;
+        if (valid) h = ((pf ? (uint32_t)cur.hi : P.u32(x)) * kHashMul) >> hsh;
         const int bk = (int)(h & (kBuckets - 1));
         if (valid) {
             atomicOr((unsigned long long *)&bmask[bk], 1ull << lane);
@@ -270,7 +285,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 } else {
                     int f = 0, c = 0;
                     if (!PL && kCap == 8) {  // 8-byte compares (writeRunlen :449-462, capped)
-                        const uint64_t df = s8(st) ^ s8(x), db = s8(st - 8) ^ s8(x - 8);
+                        const uint64_t df = s8(st) ^ (pf ? cur.hi : s8(x)), db = s8(st - 8) ^ (pf ? cur.lo : s8(x - 8));
                         f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
                         if (f > n - x) f = (int)(n - x);
                         c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
@@ -292,7 +307,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 uint64_t rb, rf;
                 const bool vec = !PL && kCap == 8 && ring8(cand - 8, wpos, rb) && ring8(cand, wpos, rf);
                 if (vec) {  // 8-byte compares against the ring image (writer.go:236-259, capped)
-                    const uint64_t db = s8(x - 8) ^ rb;
+                    const uint64_t db = (pf ? cur.lo : s8(x - 8)) ^ rb;
                     c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
                     if (c > x - done) c = (int)(x - done);
                     ist -= c;
@@ -304,7 +319,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 int64_t iend = x, end = cand;
                 int f = 0;
                 if (vec) {
-                    const uint64_t df = s8(x) ^ rf;
+                    const uint64_t df = (pf ? cur.hi : s8(x)) ^ rf;
                     f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
                     if (f > n - x) f = (int)(n - x);
                     iend += f;
