@@ -142,6 +142,10 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     uint64_t *bmask = (uint64_t *)(smem + ht_bytes);
     uint32_t *H = (uint32_t *)(smem + ht_bytes + kMaskBytes);
     uint32_t *lw = (uint32_t *)(smem + ht_bytes + kMaskBytes + kHashBytes);
+    // FP: beside every table entry, the 16 stream bytes around the position it holds
+    // (x-8 .. x+7), so that a candidate is judged without loading its bytes
+    constexpr bool FP = HTL && !RING && !PL;
+    V16 *fp = (V16 *)(smem + ht_bytes + kMaskBytes + kHashBytes);
     uint32_t *ht;
     if (HTL) ht = (uint32_t *)smem;
     else ht = RING ? A.ht_global : A.ht_global + (uint64_t)blockIdx.x * (uint64_t)hs;
@@ -225,6 +229,12 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     };
     V16 nxt_w{0, 0};
     int64_t nxt_i = -1;
+    const bool usefp = FP && pf && start == 0;
+    if (usefp) {  // the zero entries hold stream position 0
+        const V16 z = around(0);
+        for (int64_t k = lane; k < hs; k += kWave) fp[k] = z;
+        __syncthreads();
+    }
 
     while (i + 4 <= n && !o.err) {
         if (++guard > guard_max) { o.err = EZ_ESTUCK; break; }
@@ -267,6 +277,13 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         }
         int64_t cand = 0;
         if (valid) cand = prev >= 0 ? (int64_t)(uint32_t)(start + i + prev) : (int64_t)ht[h];
+        // the candidate's bytes cand-8 .. cand+7 (usefp): an earlier lane's, or the table's
+        V16 cv{0, 0};
+        if (usefp) {
+            const int src = prev >= 0 ? prev : lane;
+            const V16 pv{(uint64_t)__shfl((long long)cur.lo, src, 64), (uint64_t)__shfl((long long)cur.hi, src, 64)};
+            if (valid) cv = prev >= 0 ? pv : fp[h];
+        }
 
         // -- per-lane capped evaluation
         int kind = kReject;
@@ -280,12 +297,13 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 // runlen (writer.go:227-231 -> writeRunlen :441-489)
                 const int64_t st = done + off;
                 v_st = st;
-                if (st + 8 < n && P.u32(st) == 0 && P.u32(st + 4) == 0) {
+                if (st + 8 < n && (usefp ? cv.hi == 0 : (P.u32(st) == 0 && P.u32(st + 4) == 0))) {
                     kind = kZero;
                 } else {
                     int f = 0, c = 0;
                     if (!PL && kCap == 8) {  // 8-byte compares (writeRunlen :449-462, capped)
-                        const uint64_t df = s8(st) ^ (pf ? cur.hi : s8(x)), db = s8(st - 8) ^ (pf ? cur.lo : s8(x - 8));
+                        const uint64_t df = (usefp ? cv.hi : s8(st)) ^ (pf ? cur.hi : s8(x));
+                        const uint64_t db = (usefp ? cv.lo : s8(st - 8)) ^ (pf ? cur.lo : s8(x - 8));
                         f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
                         if (f > n - x) f = (int)(n - x);
                         c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
@@ -304,8 +322,15 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 // window match (writer.go:233-301)
                 int64_t ist = x - 1, st = cand - 1;
                 int c = 0;
-                uint64_t rb, rf;
-                const bool vec = !PL && kCap == 8 && ring8(cand - 8, wpos, rb) && ring8(cand, wpos, rf);
+                uint64_t rb = 0, rf = 0;
+                bool vec;
+                if (usefp && cand - 8 >= start && cand + 8 <= wpos && cand - 8 >= wpos - bs) {
+                    rb = cv.lo;  // block[y & mask] is stream byte y for wpos - bs <= y < wpos
+                    rf = cv.hi;
+                    vec = true;
+                } else {
+                    vec = !PL && kCap == 8 && ring8(cand - 8, wpos, rb) && ring8(cand, wpos, rf);
+                }
                 if (vec) {  // 8-byte compares against the ring image (writer.go:236-259, capped)
                     const uint64_t db = (pf ? cur.lo : s8(x - 8)) ^ rb;
                     c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
@@ -399,7 +424,10 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
 
         // -- hash inserts of the visited lanes 0..last, last writer wins (writer.go:216-217)
         const int last = a < 0 ? nvalid - 1 : a;
-        if (valid && lane <= last && next > last) ht[h] = (uint32_t)(start + x);
+        if (valid && lane <= last && next > last) {
+            ht[h] = (uint32_t)(start + x);
+            if (usefp) fp[h] = cur;
+        }
         if (valid) bmask[bk] = 0;
         __syncthreads();
 
@@ -417,7 +445,16 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
             put_hdr(o, hh, lane);
             if (xa + 1 + 4 <= n) {
                 const uint32_t h1 = (P.u32(xa + 1) * kHashMul) >> hsh;
-                if (lane == 0) ht[h1] = (uint32_t)(start + xa + 1);
+                V16 c1{0, 0};
+                if (usefp) {
+                    const int src = a + 1 < kWave ? a + 1 : a;
+                    c1 = V16{(uint64_t)__shfl((long long)cur.lo, src, 64), (uint64_t)__shfl((long long)cur.hi, src, 64)};
+                    if (a + 1 >= kWave) c1 = around(xa + 1);
+                }
+                if (lane == 0) {
+                    ht[h1] = (uint32_t)(start + xa + 1);
+                    if (usefp) fp[h1] = c1;
+                }
                 __syncthreads();
             }
             i = ienda;
@@ -482,6 +519,11 @@ __global__ __launch_bounds__(64) void k1_compress(CompressArgs A) {
 
 template <bool PL, bool HTL, bool RING>
 hipError_t launch_variant(const CompressArgs &a, hipStream_t st, size_t lds, unsigned grid) {
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void *)k1_compress<PL, HTL, RING>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_done = true;
+    }
     hipLaunchKernelGGL((k1_compress<PL, HTL, RING>), dim3(grid), dim3(64), lds, st, a);
     return hipGetLastError();
 }
@@ -540,6 +582,7 @@ hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     const bool ring = a.ring != nullptr;
     size_t lds = (htl ? (size_t)a.hs * 4 : 0) + kMaskBytes + kHashBytes;
     if (pl) lds += ((a.max_len + 3) / 4 + 8) * 4;
+    if (htl && !ring && !pl) lds += (size_t)a.hs * 16;  // candidate fingerprints
     lds = (lds + 15) & ~(size_t)15;
     uint64_t grid = a.count;
     if (!htl && !ring) grid = grid < 2048 ? grid : 2048;  // global scratch hash tables
