@@ -176,17 +176,25 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
                 if (c.cp) ok = ok && (c.D == 0 || (cs + c.L <= pos && cs >= pos + total + 16 - kWR)) && (bsl >= 30 || c.D <= (1u << bsl));
                 else ok = ok && i + lane + c.j + c.L <= in_hi;
             }
-            if (__ballot(!ok) == 0 && (uint32_t)pos + (uint32_t)total <= (uint32_t)cap) {
-                for (int32_t k = 0; __ballot(tok && 16 * k < c.L) != 0; k++) {
-                    if (tok && 16 * k < c.L) {
+            // the steps before the first one that cannot go (a copy reading this batch's
+            // output, say) run now; the next batch starts at that one
+            const uint64_t bad = __ballot(st && !ok);
+            const int32_t pf = bad ? (int32_t)__builtin_ctzll(bad) : pe;
+            // (a short prefix costs a whole scan per few steps: then step by step instead)
+            const int nrun = pf >= 64 ? 64 : __builtin_popcountll(M & ((1ull << pf) - 1));
+            if ((pf == pe || nrun >= 4) && (uint32_t)pos + (uint32_t)total <= (uint32_t)cap) {
+                const bool run = tok && lane < pf;
+                for (int32_t k = 0; __ballot(run && 16 * k < c.L) != 0; k++) {
+                    if (run && 16 * k < c.L) {
                         V16 v{0, 0};  // a zero region's
                         if (!c.cp) v = rld<kWIn>(inb, i + lane + c.j + 16 * k);
                         else if (c.D != 0) v = rld<kWR>(ring, cs + 16 * k);
                         rput<kWR>(ring, dst + 16 * k, v, (uint32_t)(c.L - 16 * k < 16 ? c.L - 16 * k : 16));
                     }
                 }
-                pos += total;
-                i += pe;
+                // output of the steps before pf: the exclusive prefix at lane pf
+                pos = pf < 64 ? __builtin_amdgcn_readlane(dst, pf) : pos + total;
+                i += pf;
                 while (pos >= fl + kWChunk) {
                     st16v(out + fl + 16 * lane, rld<kWR>(ring, fl + 16 * lane));
                     fl += kWChunk;
