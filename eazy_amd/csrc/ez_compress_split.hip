@@ -575,6 +575,13 @@ int split_g() {
     static const int g = getenv("EZ_K1S_G") ? atoi(getenv("EZ_K1S_G")) : 16;
     return g == 8 ? 8 : 16;
 }
+// lanes per stream for T32: 32 when the batch has few streams (long Writes, C2: two
+// waves per SIMD instead of one, 33.3 vs 34.3 ms); EZ_K1S_G32=16|32 overrides
+int split_g32(uint64_t count) {
+    static const int g = getenv("EZ_K1S_G32") ? atoi(getenv("EZ_K1S_G32")) : 0;
+    if (g == 32 || g == 16) return g;
+    return count <= 8192 ? 32 : split_g();
+}
 bool g_split_t32 = false;  // ez_select_compress_kernel('S')
 bool split_t32_forced() {
     static const bool v = getenv("EZ_K1S_T") && atoi(getenv("EZ_K1S_T")) == 32;
@@ -660,12 +667,14 @@ hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipSt
     const int G = split_g(), T = split_table(a);
     if (a.write_idx) {  // multi-Write streams: inputs through L1/L2
         if (T == 16) return G == 8 ? launch_split_g<8, true, true, true>(a, recs, st) : launch_split_g<16, true, true, true>(a, recs, st);
+        if (split_g32(a.count) == 32) return launch_split_g<32, false, true, true>(a, recs, st);
         return G == 8 ? launch_split_g<8, false, true, true>(a, recs, st) : launch_split_g<16, false, true, true>(a, recs, st);
     }
     // EZ_K1S_GIN=0 (experiments): inputs staged in LDS when they fit
     const bool lds_in = !split_gin() && (G == 8 ? split_stride<8, true, false>(a) : split_stride<16, true, false>(a)) != 0;
     if (T == 16 && lds_in) return G == 8 ? launch_split_g<8, true, false, false>(a, recs, st) : launch_split_g<16, true, false, false>(a, recs, st);
     if (T == 16) return G == 8 ? launch_split_g<8, true, true, false>(a, recs, st) : launch_split_g<16, true, true, false>(a, recs, st);
+    if (split_g32(a.count) == 32) return launch_split_g<32, false, true, false>(a, recs, st);
     return G == 8 ? launch_split_g<8, false, true, false>(a, recs, st) : launch_split_g<16, false, true, false>(a, recs, st);
 }
 
