@@ -83,17 +83,24 @@ __global__ __launch_bounds__(kThreads) void k3_scan3(const uint64_t *sizes, uint
 }
 
 __global__ __launch_bounds__(256) void k3_gather(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes,
-                                                 uint64_t count, uint8_t *packed, const uint64_t *packed_off) {
+                                                 uint64_t count, uint8_t *packed, const uint64_t *packed_off,
+                                                 uint32_t split) {
     const int lane = lane_id();
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / kWave);
-    for (uint64_t s = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6); s < count; s += waves) {
+    const uint64_t work = count * split;
+    for (uint64_t v = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6); v < work; v += waves) {
+        // virtual wave v = stream s, part j of split: part j moves dwords
+        // j*64 .. j*64+63 of every split*64-dword round; part 0 also the
+        // head and tail bytes
+        const uint64_t s = v / split;
+        const uint32_t j = (uint32_t)(v - s * split);
         const uint8_t *src = slots + slot_off[s];
         uint8_t *dst = packed + packed_off[s];
         const uint64_t n = sizes[s];
         // head bytes until dst is 4-aligned, then whole dwords built from
         // two aligned source dwords, then the tail bytes
         const uint64_t head = ((4 - ((uintptr_t)dst & 3)) & 3) < n ? ((4 - ((uintptr_t)dst & 3)) & 3) : n;
-        if ((uint64_t)lane < head) dst[lane] = src[lane];
+        if (j == 0 && (uint64_t)lane < head) dst[lane] = src[lane];
         const uint64_t body = (n - head) / 4;
         const uint8_t *s2 = src + head;
         const uint32_t r = (uint32_t)((uintptr_t)s2 & 3);
@@ -101,13 +108,13 @@ __global__ __launch_bounds__(256) void k3_gather(const uint8_t *slots, const uin
         uint32_t *dw = (uint32_t *)(dst + head);
         // last source word index that holds a byte of this stream
         const uint64_t wlast = (r + (n - head) + 3) / 4 - 1;
-        for (uint64_t k = lane; k < body; k += kWave) {
+        for (uint64_t k = (uint64_t)j * kWave + lane; k < body; k += (uint64_t)split * kWave) {
             const uint32_t w0 = sw[k];
             const uint32_t w1 = sw[k + 1 <= wlast ? k + 1 : wlast];
             dw[k] = __builtin_amdgcn_alignbyte(w1, w0, r);
         }
         const uint64_t t0 = head + body * 4;
-        if ((uint64_t)lane < n - t0) dst[t0 + lane] = src[t0 + lane];
+        if (j == 0 && (uint64_t)lane < n - t0) dst[t0 + lane] = src[t0 + lane];
     }
 }
 
@@ -126,10 +133,15 @@ hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uin
     hipLaunchKernelGGL(k3_scan1, dim3((unsigned)tiles), dim3(kThreads), 0, st, sizes, count, tile_sums);
     hipLaunchKernelGGL(k3_scan2, dim3(1), dim3(kThreads), 0, st, tile_sums, tiles);
     hipLaunchKernelGGL(k3_scan3, dim3((unsigned)tiles), dim3(kThreads), 0, st, sizes, count, tile_sums, packed_off);
-    uint64_t blocks = (count + 3) / 4;
+    // few (long) streams: several waves per stream so the gather fills the
+    // chip (64 streams of 4 MiB were 64 waves, 7.3 ms); 16 Ki waves in all
+    uint32_t split = 1;
+    if (count < 16384) split = (uint32_t)(16384 / count);
+    if (split > 1024) split = 1024;
+    uint64_t blocks = (count * split + 3) / 4;
     if (blocks > 65536) blocks = 65536;
     hipLaunchKernelGGL(k3_gather, dim3((unsigned)blocks), dim3(256), 0, st, slots, slot_off, sizes, count, packed,
-                       packed_off);
+                       packed_off, split);
     return hipGetLastError();
 }
 
