@@ -36,6 +36,7 @@ constexpr int32_t kRingStride = kRing + 16;  // + the mirror of bytes 0..15
 constexpr int32_t kNear = kRing - 16;    // copies this close read the ring
 constexpr int kRingBlock = 256;          // lanes per block (one wave per SIMD of a CU)
 constexpr int32_t kChunk = 128;          // output leaves the ring in whole 128-byte lines
+constexpr uint32_t kMaxFlushPer = 16;    // kChunk + 16 * (16 + 1) < kRing
 
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 
@@ -63,7 +64,8 @@ __host__ __device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v
 
 // decodes stream s with `ring` (kRingStride bytes) as its history; false = hand
 // the stream over (host-compilable: tools/ring_emu.hip runs it on the CPU)
-__host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring) {
+// fper: iterations between flushes (a power of two <= kMaxFlushPer)
+__host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring, uint32_t fper = 8) {
     const uint8_t *b = A.in + A.in_off[s];
     const int64_t nb64 = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
     const uint8_t *in_end = A.in + A.in_off[A.count];  // loads never pass the last stream's end
@@ -83,6 +85,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     if (!slow) h = ld_in(b, A.in, in_end);
     // the token being written: rem bytes at dst from sp (input / HBM output) or from the ring
     int32_t rem = 0, dst = 0, step = 16, rp = 0, fl = 0;  // fl: output below it is in HBM
+    uint32_t it = 0;
     const uint8_t *sp = b;
     bool from_in = false, patt = false, near = false;
     V16 pv{0, 0};
@@ -138,8 +141,14 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             sp += kk;
             rp += kk;
             rem -= kk;
-            // a finished 128-byte chunk of output leaves the ring as one whole line
-            if (dst >= fl + kChunk) {
+        }
+        // finished 128-byte chunks of output leave the ring as whole lines, every fper-th
+        // iteration: the lanes of a wave iterate together, so the flush is one wave-wide
+        // block every fper iterations with many lanes active, not one nearly every
+        // iteration for the few lanes that just finished a chunk (unflushed output stays
+        // below kChunk + 16 * (fper + 1) <= kRing bytes)
+        if ((++it & (fper - 1)) == 0) {
+            while (dst >= fl + kChunk) {
 #pragma unroll
                 for (int32_t t = 0; t < kChunk; t += 16) st16v(out + fl + t, ring_ld(ring, fl + t));
                 fl += kChunk;
@@ -160,14 +169,14 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
 
 // spw: streams per wave (lanes spw..63 idle): fewer streams per wave put more
 // waves on each SIMD within the same LDS
-__global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A, uint32_t spw) {
+__global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A, uint32_t spw, uint32_t fper) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (l >= spw) return;
     uint8_t *ring = smem + (w * spw + l) * kRingStride;
     const uint64_t per_block = (uint64_t)(kRingBlock / 64) * spw;
     for (uint64_t s = (uint64_t)blockIdx.x * per_block + w * spw + l; s < A.count; s += (uint64_t)gridDim.x * per_block)
-        if (!ring_one(A, s, ring)) {
+        if (!ring_one(A, s, ring, fper)) {
             const uint32_t at = atomicAdd(&A.slow[0], 1u);
             A.slow[1 + at] = (uint32_t)s;
         }
@@ -185,7 +194,12 @@ hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t st) {
     }
     const uint64_t per_block = (uint64_t)(kRingBlock / 64) * spw;
     const uint64_t grid = (a.count + per_block - 1) / per_block;
-    hipLaunchKernelGGL(k2_ring, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a, spw);
+    // EZ_K2R_FLUSH (A/B): iterations between ring flushes, a power of two <= kMaxFlushPer
+    static const uint32_t fper = [] {
+        const uint32_t v = getenv("EZ_K2R_FLUSH") ? (uint32_t)atoi(getenv("EZ_K2R_FLUSH")) : 8u;
+        return v >= 1 && v <= kMaxFlushPer && (v & (v - 1)) == 0 ? v : 8u;
+    }();
+    hipLaunchKernelGGL(k2_ring, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a, spw, fper);
     return hipGetLastError();
 }
 
