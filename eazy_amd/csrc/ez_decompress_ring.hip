@@ -32,7 +32,8 @@ namespace ez {
 namespace {
 
 constexpr int32_t kRing = 512;           // ring bytes per stream (power of two)
-constexpr int32_t kRingStride = kRing + 16;  // + the mirror of bytes 0..15
+// per lane: a 16-byte front guard, the ring, the mirror of bytes 0..15, a 16-byte back guard
+constexpr int32_t kRingStride = 16 + kRing + 16 + 16;
 constexpr int32_t kNear = kRing - 16;    // copies this close read the ring
 constexpr int kRingBlock = 256;          // lanes per block (one wave per SIMD of a CU)
 constexpr int32_t kChunk = 128;          // output leaves the ring in whole 128-byte lines
@@ -48,21 +49,21 @@ __host__ __device__ __forceinline__ V16 ring_ld(const uint8_t *ring, int32_t p) 
     const uint8_t *q = ring + (p & (kRing - 1));
     return V16{*(const u64_ua *)q, *(const u64_ua *)(q + 8)};
 }
-// 16 bytes of output position p into the ring, keeping the mirror equal to bytes 0..15
+// 16 bytes of output position p into the ring, keeping the mirror equal to bytes 0..15,
+// branch-free: the same 16 bytes are written a second time at r - kRing when they wrap
+// (their head lands in the front guard, their tail at the ring's start) or at r + kRing
+// when they start in the first 16 bytes (their head lands in the mirror, their tail in
+// the back guard), else again at r
 __host__ __device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v) {
     const int32_t r = p & (kRing - 1);
+    const int32_t r2 = r + 16 > kRing ? r - kRing : (r < 16 ? r + kRing : r);
     *(u64_ua *)(ring + r) = v.lo;
     *(u64_ua *)(ring + r + 8) = v.hi;
-    if (r + 16 > kRing) put_small(ring, shr16(v, (uint32_t)(kRing - r)), (uint32_t)(r + 16 - kRing));
-    if (r == 0) {
-        *(u64_ua *)(ring + kRing) = v.lo;
-        *(u64_ua *)(ring + kRing + 8) = v.hi;
-    } else if (r < 16) {
-        put_small(ring + kRing + r, v, (uint32_t)(16 - r));  // (put_small takes < 16 bytes)
-    }
+    *(u64_ua *)(ring + r2) = v.lo;
+    *(u64_ua *)(ring + r2 + 8) = v.hi;
 }
 
-// decodes stream s with `ring` (kRingStride bytes) as its history; false = hand
+// decodes stream s with `ring` (kRing + 16 bytes, with 16-byte guards on both sides) as its history; false = hand
 // the stream over (host-compilable: tools/ring_emu.hip runs it on the CPU)
 // fper: iterations between flushes (a power of two <= kMaxFlushPer)
 __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring, uint32_t fper = 8) {
@@ -76,7 +77,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     // 32-bit positions; clamped loads need >= 16 input bytes in the batch and a 16-byte slot
     bool slow = in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16;
     const int32_t nb = slow ? 0 : (int32_t)nb64, cap = (int32_t)cap64;
-    for (int32_t k = 0; k < kRingStride; k += 16) {
+    for (int32_t k = 0; k < kRing + 16; k += 16) {
         *(u64_ua *)(ring + k) = 0;
         *(u64_ua *)(ring + k + 8) = 0;
     }
@@ -173,7 +174,7 @@ __global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A, uint32_t
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
     if (l >= spw) return;
-    uint8_t *ring = smem + (w * spw + l) * kRingStride;
+    uint8_t *ring = smem + (w * spw + l) * kRingStride + 16;
     const uint64_t per_block = (uint64_t)(kRingBlock / 64) * spw;
     for (uint64_t s = (uint64_t)blockIdx.x * per_block + w * spw + l; s < A.count; s += (uint64_t)gridDim.x * per_block)
         if (!ring_one(A, s, ring, fper)) {

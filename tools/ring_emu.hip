@@ -39,7 +39,7 @@ int main(int argc, char **argv) {
     a.count = count;
     alignas(16) static uint8_t ring[1024];
     for (uint64_t s = 0; s < count; s++)
-        if (!ez::ring_one(a, s, ring)) size[s] = ~0ull;
+        if (!ez::ring_one(a, s, ring + 16)) size[s] = ~0ull;  // front guard
     FILE *fo = std::fopen(argv[4], "wb");
     for (uint64_t s = 0; s < count; s++)
         if (size[s] != ~0ull) std::fwrite(out.data() + out_off[s], 1, size[s], fo);
