@@ -41,6 +41,15 @@ constexpr uint32_t kMaxFlushPer = 16;    // kChunk + 16 * (16 + 1) < kRing
 
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 
+// bytes a run of period per (1..15) advances per 16-byte pattern store: the largest
+// multiple of per <= 16 (per 0, the zero region: 16), from a nibble table
+__host__ __device__ constexpr uint64_t run_steps() {
+    uint64_t k = 0;
+    for (uint32_t per = 0; per < 16; per++) k |= (uint64_t)((per ? per * (16 / per) : 16) - 1) << (4 * per);
+    return k;
+}
+__host__ __device__ __forceinline__ int32_t run_step(uint32_t per) { return (int32_t)((run_steps() >> (4 * per)) & 15) + 1; }
+
 // 16 bytes at y of the batch [lo, hi) (bytes from hi on read as 0)
 __host__ __device__ __forceinline__ V16 ld_in(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
     return y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
@@ -97,7 +106,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             const int r = k2_parse(h, i, nb, pos, cap, lim32, limit, bsl, t);
             if (r == kParseHandOver) { slow = true; break; }  // the exact decoder takes the stream
             const int32_t adv = t.adv;
-            if (r == kParseToken) {
+            {  // the token's state, set by every step (a padding or meta step has L = 0: no move)
                 const int32_t L = t.L;
                 const uint32_t j = (uint32_t)t.j, D = t.D;
                 const bool cp = t.cp;
@@ -108,23 +117,14 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
                 near = cp && D <= kNear;
                 rp = dst - (int32_t)D;
                 sp = cp ? out + rp : b + (i + (int32_t)j);
-                patt = cp && D < 16;
-                step = 16;
-                if (!cp && (int32_t)j + L <= 16) {  // a short literal is in the header's 16 bytes already
-                    patt = true;
-                    pv = shr16(h, j);
-                }
-                if (patt && cp) {
-                    // zero region (D == 0, reader.go:176-179) or a short-period run:
-                    // one 16-byte pattern stored every `step` bytes
-                    if (D == 0) {
-                        pv = V16{0, 0};
-                    } else {
-                        const uint32_t per = (uint32_t)D;
-                        pv = run_pattern(shr16(ring_ld(ring, dst - 16), 16 - per), per);
-                        step = (int32_t)(per * (16 / per));
-                    }
-                }
+                // zero region (D == 0, reader.go:176-179) or a short-period run: one 16-byte
+                // pattern stored every `step` bytes; a short literal is in the header's 16
+                // bytes already
+                const bool run = cp && D < 16;
+                patt = run || (!cp && (int32_t)j + L <= 16);
+                step = run ? run_step(D) : 16;
+                pv = shr16(h, j);
+                if (run) pv = run_pattern(shr16(ring_ld(ring, dst - 16), 16 - D), D);  // D == 0: zeros
             }
             i += adv;
             // the next header, loaded beside this token's first move
