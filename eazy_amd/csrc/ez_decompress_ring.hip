@@ -131,11 +131,13 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             if (i < nb) h = ld_in(b + i, A.in, in_end);
         }
         if (rem > 0) {
-            V16 v;
-            if (patt) v = pv;
-            else if (near) v = ring_ld(ring, rp);
-            else if (from_in ? sp + 16 > in_end : sp < out) v = from_in ? ld_clamped(sp, A.in, in_end) : ld_clamped(sp, out, out + cap);
-            else v = ld16v(sp);
+            // the ring read is taken by every lane (one LDS read, no branch level); only far
+            // copies and long literals load from HBM
+            V16 v = patt ? pv : ring_ld(ring, rp);
+            if (!patt && !near) {
+                if (from_in ? sp + 16 > in_end : sp < out) v = from_in ? ld_clamped(sp, A.in, in_end) : ld_clamped(sp, out, out + cap);
+                else v = ld16v(sp);
+            }
             ring_st(ring, dst, v);
             const int32_t kk = rem < step ? rem : step;
             dst += kk;
