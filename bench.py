@@ -65,6 +65,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
+    ap.add_argument("--e2e-chunks", type=int, default=4, help="stream chunks of the overlapped host-memory measurement")
     ap.add_argument("--stream-bytes", type=int, default=0, help="override the workload's stream size (experiments)")
     ap.add_argument("--no-check", action="store_true", help="skip the round-trip checks (timing experiments only)")
     ap.add_argument("--same", action="store_true", help="every stream a copy of stream 0 (divergence experiments)")
@@ -157,6 +158,113 @@ def e2e(ez, data, off, cb, packed, poff, ws, dws, out, osz, ost, block, htable, 
     gib = total / 2**30
     return {"compress_GiBps": gib / t["compress"], "decompress_GiBps": gib / t["decompress"],
             "note": "pinned host -> HBM -> kernels -> pinned host, hipMemcpyAsync on the compute stream, one rank"}
+
+
+def e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, block, htable, size, total, comp_bytes,
+                  chunks=4, reps=5):
+    """The host-memory path with the copies overlapped: the batch is cut into `chunks`
+    runs of whole streams; chunk k+1's host->HBM copy (one copy stream), chunk k's
+    kernels (the compute stream) and chunk k-1's HBM->host copy (a second copy
+    stream) run at once.  Chunk offsets are absolute (in_off / slot_off / out_off
+    views), so the kernels see sub-batches of the same buffers.  The packed bytes of
+    the chunks, back to back, are the one-batch packing; both are checked."""
+    import numpy as np
+    import torch
+
+    count = len(offs) - 1
+    bounds = [count * k // chunks for k in range(chunks + 1)]
+    h_in = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    h_in.copy_(data[:total].cpu())
+    h_ref = packed[:comp_bytes].cpu()
+    h_packed = torch.empty(comp_bytes, dtype=torch.uint8, pin_memory=True)
+    h_out = torch.empty(total, dtype=torch.uint8, pin_memory=True)
+    h_size = torch.zeros(chunks, dtype=torch.int64, pin_memory=True)
+    d_in = torch.empty_like(data)
+    d_packed = torch.empty_like(packed)
+    slot_host = cb.slot_off.cpu().numpy()
+    comp = torch.cuda.current_stream()
+    up, down = torch.cuda.Stream(), torch.cuda.Stream()
+    ws = [torch.empty(ez._lib().ez_pack_workspace(bounds[k + 1] - bounds[k]), dtype=torch.uint8, device=data.device)
+          for k in range(chunks)]
+    pofs = [torch.empty(bounds[k + 1] - bounds[k] + 1, dtype=torch.int64, device=data.device) for k in range(chunks)]
+    # the decompress side knows each chunk's framing (compressed sizes) as a reader would
+    pk_host = [0]
+
+    def comp_run():
+        ev_c = []
+        hb = 0
+        done_c = 0
+
+        def drain(k):
+            nonlocal hb
+            ev_c[k].synchronize()
+            n = int(h_size[k])
+            base = int(slot_host[bounds[k]])
+            with torch.cuda.stream(down):
+                h_packed[hb : hb + n].copy_(packed[base : base + n], non_blocking=True)
+            hb += n
+
+        for k in range(chunks):
+            a, b = bounds[k], bounds[k + 1]
+            lo, hi = int(offs[a]), int(offs[b])
+            e_in = torch.cuda.Event()
+            with torch.cuda.stream(up):
+                d_in[lo:hi].copy_(h_in[lo:hi], non_blocking=True)
+                e_in.record()
+            comp.wait_event(e_in)
+            sub = ez.CompressedBatch(cb.slots, cb.slot_off[a : b + 1], cb.sizes[a:b], cb.status[a:b])
+            ez.compress_batch(d_in, off[a : b + 1], block, htable, max_len=size, out=sub)
+            base = int(slot_host[a])
+            ez.pack(sub, packed[base:], pofs[k], ws[k])
+            h_size[k : k + 1].copy_(pofs[k][-1:], non_blocking=True)
+            e = torch.cuda.Event()
+            e.record()
+            down.wait_event(e)
+            ev_c.append(e)
+            if k >= 1:
+                drain(k - 1)
+        drain(chunks - 1)
+        pk_host[0] = hb
+        comp.wait_stream(down)  # the next run's kernels start after this run's copies out
+
+    def decomp_run():
+        hb = 0
+        for k in range(chunks):
+            a, b = bounds[k], bounds[k + 1]
+            n = int(h_size[k])
+            base = int(slot_host[a])
+            e_in = torch.cuda.Event()
+            with torch.cuda.stream(up):
+                d_packed[base : base + n].copy_(h_packed[hb : hb + n], non_blocking=True)
+                e_in.record()
+            hb += n
+            comp.wait_event(e_in)
+            ez.decompress_batch(d_packed[base:], pofs[k], off[a : b + 1], out=out, sizes=osz[a:b], status=ost[a:b],
+                                workspace=dws, max_len=size)
+            e = torch.cuda.Event()
+            e.record()
+            down.wait_event(e)
+            lo, hi = int(offs[a]), int(offs[b])
+            with torch.cuda.stream(down):
+                h_out[lo:hi].copy_(out[lo:hi], non_blocking=True)
+        comp.wait_stream(down)
+
+    t = {}
+    for name, f in (("compress", comp_run), ("decompress", decomp_run)):
+        f()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(reps):
+            f()
+        torch.cuda.synchronize()
+        t[name] = (time.perf_counter() - t0) / reps
+    assert pk_host[0] == comp_bytes and bool(torch.equal(h_packed, h_ref)), "chunked packing differs"
+    assert bool(torch.equal(h_out, h_in)), "pipelined host round trip differs"
+    assert int(cb.status.abs().sum()) == 0 and int(ost.abs().sum()) == 0, "pipelined statuses"
+    gib = total / 2**30
+    return {"compress_GiBps": gib / t["compress"], "decompress_GiBps": gib / t["decompress"], "chunks": chunks,
+            "note": "copies overlapped with the kernels: host->HBM, kernels and HBM->host of consecutive stream "
+                    "chunks on three HIP streams, one rank"}
 
 
 def main():
@@ -301,6 +409,9 @@ def main():
     }
     if not args.no_e2e:
         res["e2e"] = e2e(ez, data, off, cb, packed, poff, ws, dws, out, osz, ost, block, htable, size, total, comp_bytes)
+        if count >= 2 * args.e2e_chunks:
+            res["e2e"]["pipelined"] = e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, block, htable,
+                                                    size, total, comp_bytes, chunks=args.e2e_chunks)
     if rank == 0 and world == 1 and not args.no_cpu:
         cb_res, first = cpu_baseline(host, offs, block, htable, args.cpu_seconds)
         s0, slots, soff, sizes = first
