@@ -9,10 +9,10 @@ rm -rf $O && mkdir -p $O
 ARGS=${BENCH_ARGS:-}
 timeout -k 10 900 python -m pytest tests -q -m gpu > $O/gpu_tests.log 2>&1
 rc=$?; echo "pytest rc=$rc"; tail -3 $O/gpu_tests.log; [ $rc -eq 0 ] || exit $rc
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu --steps 10 --warmup 2 $ARGS > $O/prof.log 2>&1
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 bench.py --no-cpu --no-e2e --steps 10 --warmup 2 $ARGS > $O/prof.log 2>&1
 rc=$?; echo "prof rc=$rc"; [ $rc -eq 0 ] || exit $rc
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 400 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$C -o run -- python3 bench.py --no-cpu --steps 3 --warmup 1 $ARGS > $O/pmc_$C.log 2>&1
+  timeout -k 10 400 rocprofv3 --pmc $C --output-format csv -d $O/pmc_$C -o run -- python3 bench.py --no-cpu --no-e2e --steps 3 --warmup 1 $ARGS > $O/pmc_$C.log 2>&1
   rc=$?; echo "pmc $C rc=$rc"; [ $rc -eq 0 ] || exit $rc
 done
 python3 tools/traffic.py $O $O/traffic.json > $O/traffic.log 2>&1
