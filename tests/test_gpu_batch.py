@@ -211,3 +211,48 @@ def test_multi_write_streams(cuda, k1_kind):
         want = orc.compress(MiB, 1024, ws)
         got = slots[so[s] : so[s] + sz[s]].tobytes()
         assert got == want, f"stream {s}: {len(ws)} Writes of {[len(w) for w in ws]}"
+
+
+def test_sub_batches_through_offset_views(cuda):
+    """offsets are absolute, so a run of whole streams [a, b) given
+    as views (in_off[a:b+1], slot_off[a:b+1], sizes[a:b], status[a:b]) is a batch of
+    its own.  Chunks compressed, packed and decompressed this way (ragged lengths, the
+    chunk seams inside the input buffer) equal the one-batch result, byte for byte."""
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(23)
+    lens = rng.integers(0, 6000, 300)
+    lens[::37] = 0
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    host = synth.logs(21, int(offs[-1]))
+    data = torch.from_numpy(host.copy()).to(cuda)
+    off = torch.from_numpy(offs).to(cuda)
+    mx = int(lens.max())
+    cb = ez.compress_batch(data, off, MiB, 1024, max_len=mx)
+    packed, poff = ez.pack(cb)
+    want = packed[: int(poff[-1])].cpu()
+
+    sub_cb = ez.CompressedBatch(torch.zeros_like(cb.slots), cb.slot_off, torch.empty_like(cb.sizes),
+                                torch.empty_like(cb.status))
+    out = torch.zeros(int(offs[-1]) + 16, dtype=torch.uint8, device=cuda)
+    osz = torch.empty(len(lens), dtype=torch.int64, device=cuda)
+    ost = torch.empty(len(lens), dtype=torch.int32, device=cuda)
+    bounds = [0, 1, 77, 78, 200, 300]
+    got = []
+    for a, b in zip(bounds[:-1], bounds[1:]):
+        sub = ez.CompressedBatch(sub_cb.slots, sub_cb.slot_off[a : b + 1], sub_cb.sizes[a:b], sub_cb.status[a:b])
+        ez.compress_batch(data, off[a : b + 1], MiB, 1024, max_len=mx, out=sub)
+        base = int(cb.slot_off[a])
+        pk = torch.zeros(int(cb.slot_off[b]) - base + 16, dtype=torch.uint8, device=cuda)
+        pk, po = ez.pack(sub, pk)
+        got.append(pk[: int(po[-1])].cpu())
+        ez.decompress_batch(pk, po, off[a : b + 1], out=out, sizes=osz[a:b], status=ost[a:b], max_len=mx)
+    torch.cuda.synchronize()
+    assert int(sub_cb.status.abs().sum()) == 0 and int(ost.abs().sum()) == 0
+    assert torch.equal(sub_cb.sizes, cb.sizes)
+    assert torch.equal(torch.cat(got), want), "chunked packing differs from the one-batch packing"
+    assert torch.equal(osz.cpu(), torch.from_numpy(lens.astype(np.int64)))
+    assert out[: int(offs[-1])].cpu().numpy().tobytes() == host.tobytes()
