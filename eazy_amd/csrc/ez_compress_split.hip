@@ -188,7 +188,7 @@ struct Pred<0, ROW> {
 // MW: streams of several Writes (CompressArgs::write_idx), else one Write each
 template <int G, bool T16, bool GIN, bool MW>
 __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
-                                                  uint64_t rcap) {
+                                                  uint64_t rcap, int prio) {
     constexpr int S = 64 / G;
     static_assert(!T16 || G <= 16, "T16 predecessor search works within 16-lane DPP rows");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -283,6 +283,9 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         const bool valid = live && lj < nvalid;
 
         // ---- visit: hash, lookup (+ insert for T32) in lane order, writer.go:213-217
+        // (the chain up to the candidate loads' issue at high wave priority: the loads leave
+        // sooner when several waves of the SIMD are ready)
+        if (prio & 1) __builtin_amdgcn_s_setprio(3);
         const uint32_t h = valid ? ((uint32_t)pxf * kHashMul) >> hsh : 0u;
         int32_t cand = 0;
         if constexpr (T16) {
@@ -303,6 +306,7 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
             P.around(cand, pcb, pcf);
             P.around(cand + 16, pc2, pc3);
         }
+        if (prio & 1) __builtin_amdgcn_s_setprio(0);
         EZ_PROF_MARK(5);
         if (valid) {
             const bool rl = cand >= done && cand < x;
@@ -377,7 +381,9 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         if (live && (err || (i + 4 > wend && wk == wlast))) live = false;
         // the next window's bytes, in flight while this window's table writes and record go out
         EZ_PROF_MARK(6);
+        if (prio & 2) __builtin_amdgcn_s_setprio(3);
         if (live) P.around(i + lj, pxb, pxf);
+        if (prio & 2) __builtin_amdgcn_s_setprio(0);
         EZ_PROF_MARK(7);
 
         // ---- T16: the lanes Go visits store their positions (the last of a hash wins)
@@ -601,7 +607,12 @@ hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st)
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
     static const size_t pad = getenv("EZ_K1S_LDSPAD") ? (size_t)atoi(getenv("EZ_K1S_LDSPAD")) : 0;
-    hipLaunchKernelGGL((k1_parse<G, T16, GIN, MW>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap);
+    // wave priority (s_setprio 3) on the chain up to the candidate loads' issue: bit 0 (default),
+    // bit 1 around the next window's load; EZ_K1S_PRIO=0|1|2|3 (A/B, same box: 3.58 / 3.52 /
+    // 3.58 / 3.53 ms at C1)
+    static const int prio = getenv("EZ_K1S_PRIO") ? atoi(getenv("EZ_K1S_PRIO")) : 1;
+    hipLaunchKernelGGL((k1_parse<G, T16, GIN, MW>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap,
+                       prio);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
