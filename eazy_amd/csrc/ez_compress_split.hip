@@ -255,8 +255,12 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
     bool live = have && !err && (n >= 4 || wk < wlast);
     int32_t guard = 4 * n + 64 + 2 * (int32_t)(wlast - wk);
     // bytes x-8 .. x+7 around this lane's position x (loaded one window ahead)
-    uint64_t pxb = 0, pxf = 0;
-    if (live) P.around(i + lj, pxb, pxf);
+    // and x+8 .. x+23 (px2, px3), loaded with them: off the table -> candidate chain
+    uint64_t pxb = 0, pxf = 0, px2 = 0, px3 = 0;
+    if (live) {
+        P.around(i + lj, pxb, pxf);
+        P.around(i + lj + 16, px2, px3);
+    }
 #if (EZ_EXP & 4)
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime(), prof_it = 0;
 #endif
@@ -274,7 +278,10 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
             i = done = wstart = wend;
             wk++;
             wend = (int32_t)(A.write_end[wk] - A.in_off[s]);
-            if (live) P.around(i + lj, pxb, pxf);
+            if (live) {
+                P.around(i + lj, pxb, pxf);
+                P.around(i + lj + 16, px2, px3);
+            }
         }
         if (live && i + 4 > wend) live = false;  // the last Write has no position left
         int32_t nvalid = wend - 3 - i < G ? wend - 3 - i : G;
@@ -300,9 +307,8 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         // ---- capped judgement (exact decision), writer.go:219-301, writeRunlen :441-463
         bool acc = false;
         int32_t info = 0;  // cand | forward count << 20 | backward count << 25 | rl << 29 | zr << 30
-        uint64_t pcb = 0, pcf = 0, pc2 = 0, pc3 = 0, px2 = 0, px3 = 0;
-        if (valid) {  // x+8 .. x+23 and the candidate's bytes, in one wait
-            P.around(x + 16, px2, px3);
+        uint64_t pcb = 0, pcf = 0, pc2 = 0, pc3 = 0;
+        if (valid) {  // the candidate's bytes, in one wait
             P.around(cand, pcb, pcf);
             P.around(cand + 16, pc2, pc3);
         }
@@ -382,7 +388,10 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         // the next window's bytes, in flight while this window's table writes and record go out
         EZ_PROF_MARK(6);
         if (prio & 2) __builtin_amdgcn_s_setprio(3);
-        if (live) P.around(i + lj, pxb, pxf);
+        if (live) {
+            P.around(i + lj, pxb, pxf);
+            P.around(i + lj + 16, px2, px3);
+        }
         if (prio & 2) __builtin_amdgcn_s_setprio(0);
         EZ_PROF_MARK(7);
 
