@@ -3,11 +3,14 @@
 A step = one pass of the hot path over one batch resident in HBM:
   K1 compress (writer.go Writer.Write per stream) -> K3 pack -> K2 decompress
   (reader.go Reader.Read to EOF per stream).
-Workload at N=1 (BASELINE.json configs[1]): 65,536 independent 4 KiB
-log-like streams, NewWriter(MiB, 1024) each.  N>1: weak scaling, every rank
-owns its own 65,536-stream shard (streams are independent: no data-path
-collective).  value = uncompressed GiB processed by all ranks
-per second (GiB = 2^30 B).
+Workload at N=1 (BASELINE.json configs[1], "c1"): 65,536 independent 4 KiB
+log-like streams, NewWriter(MiB, 1024) each.  N>1 (configs[3], "c3"): ONE
+global batch of 1,048,576 x 4 KiB streams split into contiguous whole-stream
+shards over the ranks (strong scaling); the step adds the one real exchange of
+the sharded path, an RCCL all-gather of per-stream compressed sizes into
+global packed offsets (eazy_amd/dist.py); gathering the packed
+payload to rank 0 is timed separately ("gather").  value = uncompressed GiB
+processed by all ranks per second (GiB = 2^30 B).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N>1 via python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
@@ -26,9 +29,13 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, chip-level parameters)
 
+METRIC = "device-resident compress+decompress GiB/s, 1 MiB block, 1/2/4/8 MI355X"  # BASELINE.json
+SHARDED = {"c3"}  # workloads whose stream count is the GLOBAL batch, split over the ranks
 WORKLOADS = {
-    # name: (streams per GPU, bytes per stream, block, htable, description)
+    # name: (streams per GPU (c3: in the whole job), bytes per stream, block, htable, description)
     "c1": (65536, 4096, 1 << 20, 1024, "c1: 65536 x 4 KiB log-like streams per GPU, block 1 MiB, htable 1024"),
+    "c3": (1 << 20, 4096, 1 << 20, 1024,
+           "c3: one batch of 1048576 x 4 KiB log-like streams sharded over the GPUs, block 1 MiB, htable 1024"),
     "c2": (4096, 256 << 10, 1 << 20, 1024, "c2: 4096 x 256 KiB log-like streams per GPU, block 1 MiB, htable 1024"),
     # C4, the gradient-wire retarget: tensor buckets bit-cast to bytes (Writes longer than the window)
     "c4": (64, 4 << 20, 1 << 20, 1024, "c4: 64 x 4 MiB fp32 N(0,1e-3) gradient buckets per GPU, block 1 MiB, htable 1024"),
@@ -45,6 +52,10 @@ def workload_bytes(name, seed, total):
 
     if name in ("c1", "c2"):
         return synth.logs(seed, total), "synthetic (seeded tlwire-like log events, eazy_amd/tools/synth.c)"
+    if name == "c3":  # streams [first, last) of the global batch (rank-independent bytes)
+        first, last, size = seed
+        return (synth.global_logs(1000, first, last, size),
+                "synthetic (seeded tlwire-like log events, eazy_amd/tools/synth.c; one global batch)")
     if name == "c4h":
         f = synth.f32(seed, total // 2)
         return (f.view(np.uint32) >> 16).astype(np.uint16).view(np.uint8), "synthetic (seeded bf16 = top half of N(0,1e-3) fp32)"
@@ -61,7 +72,8 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", default="c1", choices=sorted(WORKLOADS))
+    ap.add_argument("--workload", default="auto", choices=["auto"] + sorted(WORKLOADS),
+                    help="auto: c1 on one GPU (BASELINE configs[1]), c3 sharded over N>1 GPUs (configs[3])")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="bounded CPU-baseline sample duration")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the host-memory (PCIe-inclusive) measurement")
@@ -70,44 +82,105 @@ def parse():
     ap.add_argument("--no-check", action="store_true", help="skip the round-trip checks (timing experiments only)")
     ap.add_argument("--same", action="store_true", help="every stream a copy of stream 0 (divergence experiments)")
     ap.add_argument("--streams", type=int, default=0, help="override the workload's stream count (experiments)")
-    ap.add_argument("--traffic-json", default=None, help="PMC-derived HBM bytes per launch (rocprofv3 pass)")
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC-derived HBM bytes per launch (tools/traffic.py); default: the committed "
+                         "profiles/traffic_<workload>.json when its kernel-source hash and shape match this run")
+    ap.add_argument("--no-gather", action="store_true", help="N>1: skip the timed payload gather to rank 0")
     return ap.parse_args()
 
 
-def cpu_baseline(host, offs, block, htable, seconds):
-    """The CPU restatement of the reference (oracle/, 'port') on a bounded
-    sample of the same workload, one stream per task over the box's CPU
-    share; also checks that the GPU's compressed bytes for that sample match."""
+def source_hash() -> str:
+    """Hash of everything that decides the kernels' code (HIP sources, headers,
+    build flags): PMC traffic measured at one hash is valid for any commit with
+    the same hash."""
+    import glob
+    import hashlib
+
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "eazy_amd", "csrc", "*"))) + [
+        os.path.join(ROOT, "include", "eazy.h"), os.path.join(ROOT, "eazy_amd", "Makefile")]
+    for f in files:
+        h.update(os.path.basename(f).encode())
+        h.update(open(f, "rb").read())
+    return h.hexdigest()[:16]
+
+
+def load_traffic(path, workload, count, size, dom):
+    """HBM bytes per launch of the dominant stage from a PMC summary
+    (FETCH_SIZE x 2 + WRITE_SIZE summed over the stage's kernels; gfx950
+    correction in tools/traffic.py) -> (bytes or None, provenance)."""
+    if path is None:
+        path = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
+        if not os.path.exists(path):
+            return None, "no committed PMC summary for this workload"
+        t = json.load(open(path))
+        key = (t.get("source_hash"), t.get("streams"), t.get("stream_bytes"))
+        if key != (source_hash(), count, size):
+            return None, f"{os.path.relpath(path, ROOT)} was measured on other kernel sources or shape"
+    elif not os.path.exists(path):
+        return None, f"{path} missing"
+    else:
+        t = json.load(open(path))
+    kern = t.get("kernels", t)
+    pre = {"k1_compress": "k1_", "k2_decompress": "k2_", "k3_pack": "k3_"}[dom]
+    vals = [v["traffic"] for k, v in kern.items() if k.startswith(pre) and v.get("traffic")]
+    src = os.path.relpath(path, ROOT) if path.startswith(ROOT) else path
+    return (sum(vals) if vals else None), f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, {src}"
+
+
+def _oracle_pass(orc, host, offs, block, htable, threads, seconds, g_packed=None, g_off=None):
+    """Chunks of 2,048 streams through the C oracle until `seconds` of CPU time
+    or the whole batch; with the GPU's packed bytes given, every stream the
+    oracle compressed is byte-compared with the GPU's (sizes and bytes)."""
     import numpy as np
 
+    count = len(offs) - 1
+    chunk = min(count, 2048)
+    done_bytes, t_c, t_d, k, checked = 0, 0.0, 0.0, 0, 0
+    while (t_c + t_d) < seconds and k < count // chunk:
+        s0 = k * chunk
+        o = (offs[s0 : s0 + chunk + 1] - offs[s0]).astype(np.int64)
+        data = host[offs[s0] : offs[s0 + chunk]]
+        n = np.diff(o)
+        slot_off = np.concatenate([[0], np.cumsum(n + (n >> 2) + 32)]).astype(np.int64)
+        t0 = time.perf_counter()
+        slots, sizes = orc.compress_batch(block, htable, data, o, slot_off, threads)
+        t1 = time.perf_counter()
+        out, osz = orc.decompress_batch(slots, slot_off, sizes, o, threads)
+        t2 = time.perf_counter()
+        assert np.array_equal(out, data), "oracle round trip failed"
+        if g_packed is not None:
+            g_sz = np.diff(g_off[s0 : s0 + chunk + 1])
+            bad = np.nonzero(g_sz != sizes)[0]
+            assert len(bad) == 0, f"stream {s0 + bad[0]}: GPU compressed size {g_sz[bad[0]]} != oracle {sizes[bad[0]]}"
+            keep = np.concatenate([np.arange(slot_off[s], slot_off[s] + sizes[s]) for s in range(chunk)])
+            got = g_packed[g_off[s0] : g_off[s0 + chunk]]
+            if not np.array_equal(slots[keep], got):
+                for s in range(chunk):
+                    w = slots[slot_off[s] : slot_off[s] + sizes[s]]
+                    g = g_packed[g_off[s0 + s] : g_off[s0 + s + 1]]
+                    assert np.array_equal(w, g), f"stream {s0 + s}: GPU compressed bytes differ from the oracle"
+            checked += chunk
+        t_c += t1 - t0
+        t_d += t2 - t1
+        done_bytes += int(o[-1])
+        k += 1
+    return done_bytes, t_c, t_d, k * chunk, checked
+
+
+def cpu_baseline(host, offs, block, htable, seconds, g_packed, g_off):
+    """The CPU restatement of the reference (oracle/, 'port') on a bounded
+    sample of the same workload, one stream per task over the box's CPU share
+    (16 threads), and again on one thread.  The multi-thread
+    pass byte-compares every stream it compressed with the GPU's bytes."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as orc
 
     threads = max(1, min(16, os.cpu_count() or 1))
     count = len(offs) - 1
-    chunk = min(count, 2048)
-    done_bytes, t_c, t_d, k = 0, 0.0, 0.0, 0
-    first = None
-    while (t_c + t_d) < seconds and k < count // chunk:
-        s0 = k * chunk
-        o = offs[s0 : s0 + chunk + 1] - offs[s0]
-        data = host[offs[s0] : offs[s0 + chunk]]
-        n = np.diff(o)
-        cap = n + (n >> 2) + 32
-        slot_off = np.concatenate([[0], np.cumsum(cap)]).astype(np.int64)
-        t0 = time.perf_counter()
-        slots, sizes = orc.compress_batch(block, htable, data, o.astype(np.int64), slot_off, threads)
-        t1 = time.perf_counter()
-        out, osz = orc.decompress_batch(slots, slot_off, sizes, o.astype(np.int64), threads)
-        t2 = time.perf_counter()
-        assert np.array_equal(out, data), "oracle round trip failed"
-        if first is None:
-            first = (s0, slots, slot_off, sizes)
-        t_c += t1 - t0
-        t_d += t2 - t1
-        done_bytes += int(o[-1])
-        k += 1
-    gib = done_bytes / 2**30
+    done, t_c, t_d, streams, checked = _oracle_pass(orc, host, offs, block, htable, threads, seconds, g_packed, g_off)
+    done1, t_c1, t_d1, streams1, _ = _oracle_pass(orc, host, offs, block, htable, 1, seconds / 2)
+    gib, gib1 = done / 2**30, done1 / 2**30
     return {
         "value": gib / (t_c + t_d),
         "unit": "GiB/s",
@@ -115,10 +188,12 @@ def cpu_baseline(host, offs, block, htable, seconds):
         "kind": "port",
         "compress_GiBps": gib / t_c,
         "decompress_GiBps": gib / t_d,
-        "sample": f"{k * chunk} of the {count} streams of this rank's batch ({done_bytes / 2**20:.0f} MiB), "
+        "single_thread": {"value": gib1 / (t_c1 + t_d1), "compress_GiBps": gib1 / t_c1, "decompress_GiBps": gib1 / t_d1,
+                          "cores": 1, "sample": f"{streams1} streams ({done1 / 2**20:.0f} MiB)"},
+        "sample": f"{streams} of the {count} streams of this rank's batch ({done / 2**20:.0f} MiB), "
         f"C restatement of writer.go/reader.go (oracle/eazy_oracle.c, -O3), fresh NewWriter/NewReaderBytes per stream, "
         f"{threads} host threads",
-    }, first
+    }, checked
 
 
 def e2e(ez, data, off, cb, packed, poff, ws, dws, out, osz, ost, block, htable, size, total, comp_bytes, reps=5):
@@ -176,6 +251,7 @@ def e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, blo
     h_in = torch.empty(total, dtype=torch.uint8, pin_memory=True)
     h_in.copy_(data[:total].cpu())
     h_ref = packed[:comp_bytes].cpu()
+    packed = torch.empty_like(packed)  # this run's own packing: the caller's one-batch result stays intact
     h_packed = torch.empty(comp_bytes, dtype=torch.uint8, pin_memory=True)
     h_out = torch.empty(total, dtype=torch.uint8, pin_memory=True)
     h_size = torch.zeros(chunks, dtype=torch.int64, pin_memory=True)
@@ -193,7 +269,7 @@ def e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, blo
     def comp_run():
         ev_c = []
         hb = 0
-        done_c = 0
+        up.wait_stream(comp)  # this run's uploads overwrite inputs the previous run's kernels read
 
         def drain(k):
             nonlocal hb
@@ -229,6 +305,7 @@ def e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, blo
 
     def decomp_run():
         hb = 0
+        up.wait_stream(comp)
         for k in range(chunks):
             a, b = bounds[k], bounds[k + 1]
             n = int(h_size[k])
@@ -267,6 +344,62 @@ def e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, blo
                     "chunks on three HIP streams, one rank"}
 
 
+def checksum(x, chunk: int = 1 << 26) -> int:
+    """Position-weighted byte checksum of a CUDA uint8 tensor (int64 wraparound
+    is fine: both sides compute it the same way)."""
+    import torch
+
+    acc = torch.zeros((), dtype=torch.int64, device=x.device)
+    for a in range(0, x.numel(), chunk):
+        v = x[a : a + chunk].to(torch.int64)
+        w = torch.arange(a, a + v.numel(), dtype=torch.int64, device=x.device) % 65521 + 1
+        acc += (v * w).sum()
+    return int(acc)
+
+
+def gather_check(ez, ezd, R, packed, goff, count_all, first_all, data, size, dev, reps=3):
+    """The optional payload gather of the sharded path, timed
+    separately: every rank's packed shard to rank 0 at its global offset.  Then
+    rank 0 decodes the gathered global batch (K2 over all streams) and compares
+    each rank's range with that rank's input by checksum."""
+    import torch
+
+    total_c = int(goff[-1])
+    out = torch.empty(total_c + 64, dtype=torch.uint8, device=dev) if R.is_root else None  # +64: decoder over-read slack
+    ts = []
+    for _ in range(reps):
+        ezd.barrier(R)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ezd.gather_payload(packed, goff, count_all, R, out=out)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    (t,) = ezd.reduce_max([min(ts)], R, dev)
+    sums = [0] * R.world
+    mine = checksum(data[: (first_all[R.rank + 1] - first_all[R.rank]) * size])
+    if R.world > 1:
+        import torch.distributed as dist
+
+        g = torch.zeros(R.world, dtype=torch.int64, device=dev)
+        g[R.rank] = mine
+        dist.all_reduce(g)
+        sums = g.tolist()
+    else:
+        sums = [mine]
+    if R.is_root:
+        in_off = torch.arange(count_all + 1, dtype=torch.int64, device=dev) * size
+        dec, dsz, dst = ez.decompress_batch(out, goff, in_off, max_len=size)
+        assert int(dst.abs().sum()) == 0, "gathered batch: decode status"
+        for k in range(R.world):
+            a, b = first_all[k] * size, first_all[k + 1] * size
+            assert checksum(dec[a:b]) == sums[k], f"gathered shard of rank {k} does not decode to its input"
+    moved = total_c - (ezd.rank_bytes(goff, count_all, R.world)[0][1])
+    return {"ms": t * 1e3, "bytes_to_root": moved, "GBps_into_root": moved / t / 1e9 if t > 0 else None,
+            "note": "grouped point-to-point sends of each rank's packed shard to rank 0 at its global offset "
+                    "(torch.distributed P2P over RCCL); rank 0 then decodes the whole gathered batch and checks "
+                    "every rank's range against that rank's input checksum"}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -285,15 +418,24 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    count, size, block, htable, desc = WORKLOADS[args.workload]
+    wl = args.workload if args.workload != "auto" else ("c1" if world == 1 else "c3")
+    count, size, block, htable, desc = WORKLOADS[wl]
     if args.stream_bytes:
         size = args.stream_bytes
         desc += f" (stream size overridden: {size} B)"
     if args.streams:
         count = args.streams
         desc += f" (stream count overridden: {count})"
+    sharded = wl in SHARDED
+    count_all = count if sharded else count * world
+    first_all = [ezd.shard_range(count_all, ezd.Rank(k, world, k))[0] for k in range(world)] + [count_all]
+    if sharded:
+        first, last = ezd.shard_range(count_all, R)
+        count = last - first
+        host, data_desc = workload_bytes(wl, (first, last, size), count * size)
+    else:
+        host, data_desc = workload_bytes(wl, 1000 + rank, count * size)  # this rank's own independent streams
     total = count * size
-    host, data_desc = workload_bytes(args.workload, ezd.seed(1000, R), total)  # this rank's shard of independent streams
     offs = synth.batch_offsets(count, size)
     if args.same:
         host = np.tile(host[:size], count)
@@ -313,6 +455,7 @@ def main():
     out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
     osz = torch.empty(count, dtype=torch.int64, device=dev)
     ost = torch.empty(count, dtype=torch.int32, device=dev)
+    goff = [None]
 
     def step(ev=None):
         if ev:
@@ -323,9 +466,13 @@ def main():
         ez.pack(cb, packed, poff, ws)
         if ev:
             ev[2].record()
-        ez.decompress_batch(packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws, max_len=size)
+        if sharded:  # the sharded path's exchange: per-stream sizes -> global packed offsets on every rank
+            goff[0] = ezd.global_offsets(ezd.exchange_sizes(poff[1:] - poff[:-1], count_all, R))
         if ev:
             ev[3].record()
+        ez.decompress_batch(packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws, max_len=size)
+        if ev:
+            ev[4].record()
 
     for _ in range(args.warmup):
         step()
@@ -335,9 +482,12 @@ def main():
         assert int(cb.status.abs().sum()) == 0, "compress status"
         assert int(ost.abs().sum()) == 0, "decompress status"
         assert bool(torch.equal(out[:total], data)), "round trip differs"
+        if sharded:
+            base = int(goff[0][first_all[rank]])
+            assert torch.equal(goff[0][first_all[rank] : first_all[rank + 1] + 1] - base, poff), "global offsets"
     comp_bytes = int(poff[-1])
 
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     ezd.barrier(R)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -349,29 +499,26 @@ def main():
     elapsed = t1 - t0
     k1 = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     k3 = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-    k2 = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
-    elapsed, k1, k2, k3 = ezd.reduce_max([elapsed, k1, k2, k3], R, dev)  # the job ends with its slowest rank
+    xch = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
+    k2 = sum(e[3].elapsed_time(e[4]) for e in evs) / args.steps
+    elapsed, k1, k2, k3, xch = ezd.reduce_max([elapsed, k1, k2, k3, xch], R, dev)  # the job ends with its slowest rank
     (comp_all,) = ezd.reduce_sum([comp_bytes], R, dev)
 
     ms = elapsed / args.steps * 1e3
-    gib_step = total * world / 2**30
+    gib_step = count_all * size / 2**30
     value = gib_step / (ms / 1e3)
     # roofline of the dominant kernel: algorithmic bytes = input n + compressed c
     kern = {"k1_compress": k1, "k2_decompress": k2, "k3_pack": k3}
     dom = max(kern, key=kern.get)
     alg = total + comp_bytes  # per launch on this rank (n + c), SURVEY.md §8d
     achieved = alg / (kern[dom] / 1e3) / 1e9
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
-        # PMC pass of the same command (tools/traffic.py): HBM bytes per launch of the dominant kernel
-        t = json.load(open(args.traffic_json))
-        pre = {"k1_compress": "k1_", "k2_decompress": "k2_", "k3_pack": "k3_"}[dom]
-        # kernels of this step in the PMC pass: the launch's traffic = sum over its kernels (K2: fast + exact)
-        vals = [v["traffic"] for k, v in t.items() if k.startswith(pre) and v.get("traffic")]
-        traffic = sum(vals) if vals else None
+    traffic, traffic_src = load_traffic(args.traffic_json, wl, count, size, dom)
 
+    par = (f"dp{world}: one global batch in contiguous whole-stream shards; RCCL all-gather of per-stream sizes "
+           f"-> global offsets in the step" if sharded else
+           f"dp{world} (independent stream shards per rank, no data-path collective)")
     res = {
-        "metric": "device-resident compress+decompress GiB/s, 1 MiB block",
+        "metric": METRIC,
         "value": value,
         "unit": "GiB/s",
         "n_gpus": world,
@@ -379,21 +526,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if sharded else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": data_desc,
         "config": {
             "workload": desc,
+            "streams_total": count_all,
             "streams_per_gpu": count,
             "stream_bytes": size,
             "block": block,
             "htable": htable,
-            "parallelism": f"dp{world} (independent stream shards, no data-path collective)",
+            "parallelism": par,
         },
         "compress_GiBps": gib_step / ((k1 + k3) / 1e3),
         "decompress_GiBps": gib_step / (k2 / 1e3),
-        "ratio": total * world / comp_all,
+        "ratio": count_all * size / comp_all,
         "kernel_ms": {"k1_compress": k1, "k3_pack": k3, "k2_decompress": k2},
         "roofline": {
             "bound": "hbm",
@@ -403,25 +551,26 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_source": traffic_src,
+            "source_hash": source_hash(),
             "algorithmic_bytes_per_launch": alg,
         },
         "cpu_baseline": None,
     }
-    if not args.no_e2e:
+    if sharded:
+        res["kernel_ms"]["size_exchange"] = xch
+        if not args.no_gather:
+            res["gather"] = gather_check(ez, ezd, R, packed, goff[0], count_all, first_all, data, size, dev)
+    if not args.no_e2e and world == 1:
         res["e2e"] = e2e(ez, data, off, cb, packed, poff, ws, dws, out, osz, ost, block, htable, size, total, comp_bytes)
         if count >= 2 * args.e2e_chunks:
             res["e2e"]["pipelined"] = e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, block, htable,
                                                     size, total, comp_bytes, chunks=args.e2e_chunks)
     if rank == 0 and world == 1 and not args.no_cpu:
-        cb_res, first = cpu_baseline(host, offs, block, htable, args.cpu_seconds)
-        s0, slots, soff, sizes = first
-        g_p = packed.cpu().numpy()
-        g_o = poff.cpu().numpy()
-        for s in range(0, len(sizes), 97):  # GPU bytes == oracle bytes on the sample
-            want = slots[soff[s] : soff[s] + sizes[s]].tobytes()
-            got = g_p[g_o[s0 + s] : g_o[s0 + s + 1]].tobytes()
-            assert got == want, f"stream {s0 + s}: GPU compressed bytes differ from the oracle"
+        cb_res, checked = cpu_baseline(host, offs, block, htable, args.cpu_seconds, packed.cpu().numpy(), poff.cpu().numpy())
         res["cpu_baseline"] = cb_res
+        res["parity"] = {"streams_byte_compared_with_oracle": checked, "streams": count,
+                         "round_trip_on_device": "all streams" if not args.no_check else "skipped"}
     if rank == 0:
         print(json.dumps(res), flush=True)
     if world > 1:

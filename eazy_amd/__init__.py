@@ -373,10 +373,12 @@ class Reader:
         p = (C.c_uint8 * max(n, 1))()
         got, err = 0, OK
         while got < n and err == OK:
-            bb = (C.c_uint8 * max(len(self._b), 1)).from_buffer_copy(bytes(self._b) or b"\0")
+            nb = len(self._b)
+            bb = (C.c_uint8 * max(nb, 1)).from_buffer(self._b if nb else bytearray(1))  # no copy of r.b
             m, i, det = C.c_size_t(), C.c_size_t(), C.c_int64()
-            err = L.ez_reader_read(self._h, bb, len(self._b), self._i, self._boff,
+            err = L.ez_reader_read(self._h, bb, nb, self._i, self._boff,
                                    C.byref(p, got), n - got, C.byref(m), C.byref(i), C.byref(det))
+            del bb  # release the export: more() resizes r.b
             if err == EDEVICE:
                 raise DeviceError(err)
             got += m.value

@@ -270,9 +270,12 @@ extern "C" int ez_writer_is_reset(const ez_writer *w) { return w->pristine ? 1 :
 
 extern "C" int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t *out, size_t cap, size_t *out_n) {
     *out_n = 0;
+    const size_t bound = ez_compress_bound(n);
+    // checked before anything reaches the device: the kernel advances the handle's ring and table, so a
+    // call that could not return its bytes must not run at all (a retry then sees the same history)
+    if (cap < bound) return EZ_ENOSPC;
     DeviceGuard g(w->device);
     if (!g.ok) return EZ_EDEVICE;
-    const size_t bound = ez_compress_bound(n);
     if (w->in.ensure(n + 16) || w->out.ensure(bound + 16) || w->meta.ensure(64)) return EZ_EDEVICE;
     // meta: in_off[2] out_off[2] out_size[1] status[1]
     uint64_t m[6] = {0, (uint64_t)n, 0, (uint64_t)bound, 0, 0};
@@ -299,10 +302,15 @@ extern "C" int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t
     EZ_HIP(ez::launch_compress(a, w->stream));
     EZ_HIP(hipMemcpyAsync(m, w->meta.p, sizeof(m), hipMemcpyDeviceToHost, w->stream));
     EZ_HIP(hipStreamSynchronize(w->stream));
-    const int st = (int)(int32_t)(m[5] & 0xffffffffu);
-    if (st) return st;
+    int st = (int)(int32_t)(m[5] & 0xffffffffu);
     const size_t got = (size_t)m[4];
-    if (got > cap) return EZ_ENOSPC;
+    if (!st && got > cap) st = EZ_ENOSPC;  // cannot happen with cap >= bound (tests/test_bound.py)
+    if (st) {
+        // the device history already holds p while the stream position does not: start the stream
+        // over, as Go does after a failed sink write (writer.go:391-393), so later Writes stay exact
+        const int z = writer_zero(w);
+        return z ? z : st;
+    }
     if (got) {
         EZ_HIP(hipMemcpyAsync(out, w->out.p, got, hipMemcpyDeviceToHost, w->stream));
         EZ_HIP(hipStreamSynchronize(w->stream));
@@ -361,7 +369,8 @@ struct ez_reader {
     ez::DecodeState st{};
     int64_t limit = 0;
     int require_magic = 0, skip_meta = 0;
-    DBuf in, out, win, tmp, dstate, meta;
+    DBuf in, obuf[2], dstate, meta;  // obuf: history + output, double-buffered (ez_reader_read)
+    int cur = 0;
     hipStream_t stream = nullptr;
 };
 
@@ -387,9 +396,8 @@ extern "C" void ez_reader_free(ez_reader *r) {
     if (!r) return;
     DeviceGuard g(r->device);
     r->in.release();
-    r->out.release();
-    r->win.release();
-    r->tmp.release();
+    r->obuf[0].release();
+    r->obuf[1].release();
     r->dstate.release();
     r->meta.release();
     if (r->stream) (void)hipStreamDestroy(r->stream);
@@ -414,6 +422,13 @@ extern "C" int ez_reader_reset(ez_reader *r) {
 
 extern "C" int ez_reader_pending(const ez_reader *r) { return r->st.state != 0 ? 1 : 0; }
 
+// Input is uploaded in windows from b[i] on, not the whole of b per call: a Read loop over one large
+// NewReaderBytes buffer then moves each input byte to the device about once.  A window that ends inside
+// a token makes the decoder stop there with EZ_ESHORTBUF and nothing of that token consumed
+// (reader.go:218-270), so the next window resumes at exactly that token; a token longer than the window
+// with no progress doubles the window.  The decoded block history sits in front of the output in one of
+// two device buffers; after a call the last min(pos, bs) bytes are copied once into the head of the
+// other buffer, which the next call decodes into.
 extern "C" int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size_t i, int64_t boff, uint8_t *p,
                               size_t p_len, size_t *n, size_t *i_out, int64_t *detail) {
     *n = 0;
@@ -423,45 +438,74 @@ extern "C" int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size
     DeviceGuard g(r->device);
     if (!g.ok) return EZ_EDEVICE;
     const size_t H = (size_t)r->st.hist;
-    if (r->in.ensure(b_len + 16) || r->out.ensure(H + p_len + 16) || r->meta.ensure(64)) return EZ_EDEVICE;
-    if (b_len) EZ_HIP(hipMemcpyAsync(r->in.p, b, b_len, hipMemcpyHostToDevice, r->stream));
-    if (H) EZ_HIP(hipMemcpyAsync(r->out.p, r->win.p, H, hipMemcpyDeviceToDevice, r->stream));
-    r->st.i = (int64_t)i;
-    EZ_HIP(hipMemcpyAsync(r->dstate.p, &r->st, sizeof(r->st), hipMemcpyHostToDevice, r->stream));
-    uint64_t m[4] = {0, (uint64_t)b_len, (uint64_t)H, (uint64_t)(H + p_len)};
-    EZ_HIP(hipMemcpyAsync(r->meta.p, m, sizeof(m), hipMemcpyHostToDevice, r->stream));
-    ez::DecompressArgs a{};
-    uint64_t *dm = r->meta.as<uint64_t>();
-    a.in = r->in.as<uint8_t>();
-    a.in_off = dm;
-    a.out = r->out.as<uint8_t>();
-    a.out_off = dm + 2;
-    a.out_size = nullptr;
-    a.status = nullptr;
-    a.count = 1;
-    a.block_size_limit = r->limit;
-    a.require_magic = r->require_magic;
-    a.skip_unsupported_meta = r->skip_meta;
-    a.handle = 1;
-    a.boff = boff;
-    a.st = r->dstate.as<ez::DecodeState>();
-    EZ_HIP(ez::launch_decompress(a, r->stream));
-    EZ_HIP(hipMemcpyAsync(&r->st, r->dstate.p, sizeof(r->st), hipMemcpyDeviceToHost, r->stream));
-    EZ_HIP(hipStreamSynchronize(r->stream));
-    const size_t got = (size_t)r->st.n;
-    const size_t H2 = (size_t)r->st.hist;
-    // keep the last min(pos, bs) bytes of the current block as history
-    if (H2) {
-        if (r->tmp.ensure(H2) || r->win.ensure(H2)) return EZ_EDEVICE;
-        EZ_HIP(hipMemcpyAsync(r->tmp.p, r->out.as<uint8_t>() + H + got - H2, H2, hipMemcpyDeviceToDevice, r->stream));
-        EZ_HIP(hipMemcpyAsync(r->win.p, r->tmp.p, H2, hipMemcpyDeviceToDevice, r->stream));
+    DBuf &cur = r->obuf[r->cur];
+    if (cur.cap < H + p_len + 16) {  // grow, keeping the history at the head
+        DBuf nb;
+        if (nb.ensure(H + p_len + 16)) return EZ_EDEVICE;
+        if (H) EZ_HIP(hipMemcpyAsync(nb.p, cur.p, H, hipMemcpyDeviceToDevice, r->stream));
+        EZ_HIP(hipStreamSynchronize(r->stream));
+        cur.release();
+        cur = nb;
+        nb.p = nullptr;
+        nb.cap = 0;
     }
-    if (got) EZ_HIP(hipMemcpyAsync(p, r->out.as<uint8_t>() + H, got, hipMemcpyDeviceToHost, r->stream));
+    if (r->meta.ensure(64)) return EZ_EDEVICE;
+    size_t win = p_len * 2 + 64 < ((size_t)1 << 16) ? ((size_t)1 << 16) : p_len * 2 + 64;
+    size_t at = i, got = 0;
+    int err = EZ_OK;
+    for (;;) {
+        const size_t take = b_len - at < win ? b_len - at : win;
+        if (r->in.ensure(take + 16)) return EZ_EDEVICE;
+        if (take) EZ_HIP(hipMemcpyAsync(r->in.p, b + at, take, hipMemcpyHostToDevice, r->stream));
+        r->st.i = 0;
+        EZ_HIP(hipMemcpyAsync(r->dstate.p, &r->st, sizeof(r->st), hipMemcpyHostToDevice, r->stream));
+        uint64_t m[4] = {0, (uint64_t)take, (uint64_t)(H + got), (uint64_t)(H + p_len)};
+        EZ_HIP(hipMemcpyAsync(r->meta.p, m, sizeof(m), hipMemcpyHostToDevice, r->stream));
+        ez::DecompressArgs a{};
+        uint64_t *dm = r->meta.as<uint64_t>();
+        a.in = r->in.as<uint8_t>();
+        a.in_off = dm;
+        a.out = cur.as<uint8_t>();
+        a.out_off = dm + 2;
+        a.out_size = nullptr;
+        a.status = nullptr;
+        a.count = 1;
+        a.block_size_limit = r->limit;
+        a.require_magic = r->require_magic;
+        a.skip_unsupported_meta = r->skip_meta;
+        a.handle = 1;
+        a.boff = boff + (int64_t)at;  // absolute offset of the window's first byte
+        a.st = r->dstate.as<ez::DecodeState>();
+        EZ_HIP(ez::launch_decompress(a, r->stream));
+        EZ_HIP(hipMemcpyAsync(&r->st, r->dstate.p, sizeof(r->st), hipMemcpyDeviceToHost, r->stream));
+        EZ_HIP(hipStreamSynchronize(r->stream));
+        err = r->st.err;
+        const size_t used = (size_t)r->st.i, made = (size_t)r->st.n;
+        at += used;
+        got += made;
+        // the window, not the input, ran short: go on with the next one
+        if (err == EZ_ESHORTBUF && take < b_len - (at - used) && got < p_len) {
+            if (used == 0 && made == 0) win *= 2;
+            continue;
+        }
+        break;
+    }
+    const size_t H2 = (size_t)r->st.hist;
+    if (got) EZ_HIP(hipMemcpyAsync(p, cur.as<uint8_t>() + H, got, hipMemcpyDeviceToHost, r->stream));
+    if (H2) {  // the next call decodes into the other buffer, behind this block's last H2 bytes
+        DBuf &nxt = r->obuf[r->cur ^ 1];
+        if (nxt.cap < H2 + 16) {
+            EZ_HIP(hipStreamSynchronize(r->stream));
+            if (nxt.ensure(H2 + 16)) return EZ_EDEVICE;
+        }
+        EZ_HIP(hipMemcpyAsync(nxt.p, cur.as<uint8_t>() + H + got - H2, H2, hipMemcpyDeviceToDevice, r->stream));
+        r->cur ^= 1;
+    }
     EZ_HIP(hipStreamSynchronize(r->stream));
     *n = got;
-    *i_out = (size_t)r->st.i;
+    *i_out = at;
     if (detail) *detail = r->st.detail;
-    return r->st.err;
+    return err;
 }
 
 // ------------------------------------------------------------------ batches

@@ -1,11 +1,25 @@
-"""Multi-GPU layout of the batch path: one process per GPU,
-each owning a contiguous shard of whole streams.  Streams share no state
-(writer.go:40-45 state is per Writer), so the data path has no collective;
-torch.distributed (RCCL on GPUs, gloo on CPU) is used only for the barrier
-around the timed region and to reduce the reported numbers.
+"""Multi-GPU data path of the batch codec: one process per GPU,
+each owning a contiguous shard of whole streams of ONE global batch.
 
-Weak scaling: every rank owns `per_rank` streams; rank r's synthetic input
-is seeded with base_seed + r, so shards are distinct and reproducible."""
+Streams share no state (the Writer's ring, table and position are per Writer,
+writer.go:40-45; a Reader's likewise, reader.go:17-40), so compression and
+decompression need no collective.  The one real exchange is the framing of
+the global result: each rank knows only its own streams' compressed sizes, and
+the packed global output (the streams back to back, as one caller would
+concatenate the independent Writers' sink outputs) needs every stream's
+global offset.  So:
+
+1. ``shard_range``: rank r owns streams [count*r//N, count*(r+1)//N).
+2. ``exchange_sizes``: an all-gather of the per-stream compressed sizes
+   (int64, padded to the largest shard; RCCL over xGMI on GPUs, gloo on the
+   CPU) gives every rank the global size table; ``global_offsets`` is its
+   exclusive scan, and a rank's shard starts at offsets[first].
+3. ``gather_payload`` (optional, timed separately by bench.py): grouped
+   point-to-point sends of each rank's packed shard to the root, received
+   in place at the shard's global offset.
+
+Tensors stay on whatever device the backend needs (CUDA for nccl/RCCL, CPU for
+gloo); nothing here copies between host and device."""
 
 from __future__ import annotations
 
@@ -30,13 +44,82 @@ def from_env() -> Rank:
                 int(os.environ.get("LOCAL_RANK", "0")))
 
 
-def shard(per_rank: int, r: Rank) -> tuple[int, int]:
-    """Global stream range [first, last) owned by rank r (weak scaling)."""
-    return r.rank * per_rank, (r.rank + 1) * per_rank
+def shard_range(count: int, r: Rank) -> tuple[int, int]:
+    """Global stream range [first, last) of rank r: contiguous, whole streams,
+    sizes differing by at most one stream (strong scaling over one batch)."""
+    return count * r.rank // r.world, count * (r.rank + 1) // r.world
 
 
-def seed(base: int, r: Rank) -> int:
-    return base + r.rank
+def shard_counts(count: int, world: int) -> list[int]:
+    return [count * (k + 1) // world - count * k // world for k in range(world)]
+
+
+def exchange_sizes(local_sizes, count: int, r: Rank):
+    """All-gather of per-stream compressed sizes (int64 tensor, this rank's
+    shard in stream order) -> the global size table (count,) on every rank."""
+    import torch
+
+    if r.world == 1:
+        return local_sizes.clone()
+    import torch.distributed as dist
+
+    counts = shard_counts(count, r.world)
+    assert local_sizes.numel() == counts[r.rank], "local sizes must cover exactly this rank's shard"
+    m = max(counts)
+    buf = torch.zeros(m, dtype=torch.int64, device=local_sizes.device)
+    buf[: local_sizes.numel()] = local_sizes
+    allb = torch.empty(r.world * m, dtype=torch.int64, device=local_sizes.device)
+    dist.all_gather_into_tensor(allb, buf)
+    return torch.cat([allb[k * m : k * m + counts[k]] for k in range(r.world)])
+
+
+def global_offsets(global_sizes):
+    """Exclusive scan: offsets[s] = global packed position of stream s (count+1)."""
+    import torch
+
+    z = torch.zeros(1, dtype=torch.int64, device=global_sizes.device)
+    return torch.cat([z, torch.cumsum(global_sizes, 0)])
+
+
+def rank_bytes(offsets, count: int, world: int) -> list[tuple[int, int]]:
+    """(base, length) of every rank's packed shard in the global output."""
+    o = offsets.cpu().tolist() if hasattr(offsets, "cpu") else list(offsets)
+    res = []
+    for k in range(world):
+        a, b = count * k // world, count * (k + 1) // world
+        res.append((int(o[a]), int(o[b]) - int(o[a])))
+    return res
+
+
+def gather_payload(packed_local, offsets, count: int, r: Rank, out=None, root: int = 0):
+    """Rank `root` receives every rank's packed shard (packed_local[:length])
+    at its global offset into `out` (allocated if None, offsets[-1] bytes);
+    other ranks send.  Returns `out` on the root, None elsewhere."""
+    import torch
+
+    spans = rank_bytes(offsets, count, r.world)
+    if r.rank == root:
+        if out is None:
+            out = torch.empty(max(1, spans[-1][0] + spans[-1][1]), dtype=torch.uint8, device=packed_local.device)
+        base, n = spans[root]
+        out[base : base + n].copy_(packed_local[:n])
+    if r.world == 1:
+        return out
+    import torch.distributed as dist
+
+    ops = []
+    if r.rank == root:
+        for k, (base, n) in enumerate(spans):
+            if k != root and n:
+                ops.append(dist.P2POp(dist.irecv, out[base : base + n], k))
+    else:
+        n = spans[r.rank][1]
+        if n:
+            ops.append(dist.P2POp(dist.isend, packed_local[:n], root))
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+    return out if r.rank == root else None
 
 
 def reduce_max(values, r: Rank, device=None) -> list[float]:

@@ -38,3 +38,18 @@ def f32(seed: int, count: int, sigma: float = 1e-3) -> np.ndarray:
 
 def batch_offsets(count: int, size: int) -> np.ndarray:
     return np.arange(count + 1, dtype=np.int64) * size
+
+
+def global_logs(seed: int, first: int, last: int, size: int, chunk: int = 65536) -> np.ndarray:
+    """Streams [first, last) of a global batch of `size`-byte log streams whose
+    chunk k (streams k*chunk .. (k+1)*chunk-1) is logs(seed + k, chunk*size):
+    every rank of a sharded run generates exactly its own streams, and the
+    bytes do not depend on the number of ranks."""
+    out = np.empty((last - first) * size, np.uint8)
+    at = 0
+    for k in range(first // chunk, (last + chunk - 1) // chunk):
+        c = logs(seed + k, chunk * size)
+        a, b = max(first, k * chunk) - k * chunk, min(last, (k + 1) * chunk) - k * chunk
+        out[at : at + (b - a) * size] = c[a * size : b * size]
+        at += (b - a) * size
+    return out

@@ -1,19 +1,21 @@
-"""N>1 layout of the batch path on the CPU (gloo, world size 2): shards are
-disjoint whole-stream ranges, the job time is the max over ranks, and the
-job's byte counts are the sum of the independent shards.
-Launched exactly like bench.py's multi-GPU path (torch.distributed.run)."""
+"""The N>1 data path at world size 2 over gloo, launched exactly
+like bench.py's multi-GPU path (torch.distributed.run): one global batch split
+into contiguous whole-stream shards, an all-gather of per-stream compressed
+sizes into global packed offsets, and the payload gathered to rank 0.  The
+gathered bytes must equal the single-rank packing of the whole batch (the
+streams' oracle bytes back to back).  The "gpu" variant compresses each shard
+with the HIP kernels on cuda:0 (two ranks sharing the one GPU of the box)."""
 
-import json
 import os
 import socket
 import subprocess
 import sys
 
 import numpy as np
+import pytest
 
 import oracle as orc
 from eazy_amd import dist as ezd
-from eazy_amd import synth
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 
@@ -26,28 +28,49 @@ def _port():
 
 def test_shard_layout_single_process():
     rs = [ezd.Rank(r, 4, r) for r in range(4)]
-    assert [ezd.shard(10, r) for r in rs] == [(0, 10), (10, 20), (20, 30), (30, 40)]
-    assert len({ezd.seed(1000, r) for r in rs}) == 4
+    assert [ezd.shard_range(10, r) for r in rs] == [(0, 2), (2, 5), (5, 7), (7, 10)]
+    assert [ezd.shard_range(1 << 20, ezd.Rank(r, 8, r))[0] for r in range(8)] == [k << 17 for k in range(8)]
+    assert ezd.shard_counts(10, 4) == [2, 3, 2, 3]
     assert ezd.reduce_max([1.5, 2], ezd.Rank(0, 1, 0)) == [1.5, 2.0]
     assert ezd.reduce_sum([3, 4], ezd.Rank(0, 1, 0)) == [3, 4]
 
 
-def test_two_rank_gloo(tmp_path):
-    out = tmp_path / "r0.json"
+def test_global_logs_rank_independent():
+    """A rank's streams of the global batch do not depend on the split."""
+    from eazy_amd import synth
+
+    whole = synth.global_logs(5, 0, 40, 64, chunk=16)
+    for a, b in ((0, 13), (13, 27), (27, 40), (16, 32)):
+        assert np.array_equal(synth.global_logs(5, a, b, 64, chunk=16), whole[a * 64 : b * 64])
+    assert np.array_equal(whole[: 16 * 64], synth.logs(5, 16 * 64))
+
+
+def _run(tmp_path, mode):
+    sys.path.insert(0, os.path.join(HERE, "helpers"))
+    import dist_worker as dw
+
     env = dict(os.environ, OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
-           os.path.join(HERE, "helpers", "dist_worker.py"), str(out)]
+           os.path.join(HERE, "helpers", "dist_worker.py"), str(tmp_path), mode]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
     assert p.returncode == 0, p.stderr[-3000:]
-    r = json.load(open(out))
-    assert r["world"] == 2 and r["ms"] == 2.0
-    assert [x[:2] for x in r["ranges"]] == [[0, 32], [32, 64]]
-    # the job's compressed bytes = the sum of each shard compressed alone
-    want = 0
-    for rank in range(2):
-        host = synth.logs(1000 + rank, 32 * 1024)
-        for s in range(32):
-            want += len(orc.compress(1 << 20, 1024, [host[s * 1024 : (s + 1) * 1024].tobytes()]))
-    assert r["comp"] == want and r["in"] == 2 * 32 * 1024
-    assert [x[2] for x in r["ranges"]] != [0, 0]
+    host, offs = dw.global_batch()
+    want = [orc.compress(1 << 20, 1024, [host[offs[s] : offs[s + 1]].tobytes()]) for s in range(dw.COUNT)]
+    sizes = np.load(tmp_path / "sizes.npy")
+    goff = np.load(tmp_path / "offsets.npy")
+    packed = np.load(tmp_path / "packed.npy").tobytes()
+    assert sizes.tolist() == [len(w) for w in want]
+    assert goff.tolist() == np.concatenate([[0], np.cumsum([len(w) for w in want])]).tolist()
+    assert packed == b"".join(want), "gathered packing differs from the single-rank packing"
+    spans = [tuple(map(int, x.split(":"))) for x in open(tmp_path / "ranges.txt").read().split()]
+    assert spans[0][0] == 0 and spans[1][0] == spans[0][1] and sum(n for _, n in spans) == len(packed)
+
+
+def test_two_rank_gloo_exchange(tmp_path):
+    _run(tmp_path, "cpu")
+
+
+@pytest.mark.gpu
+def test_two_rank_exchange_gpu_kernels(tmp_path, cuda):
+    _run(tmp_path, "gpu")

@@ -1,0 +1,145 @@
+"""GPU parity at the BASELINE configurations other than C1 (SURVEY.md §8, configs
+C2 and C4), and the long token forms, through the C-ABI (include/eazy.h).
+
+* C2 — 256 KiB log Writes into NewWriter(MiB, 1024): K1s-T32 (the automatic
+  choice at this shape) and the general K1 forced.
+* C4 — gradient buckets bit-cast to bytes: fp32 N(0, 1e-3), bf16 (its top
+  halves), 90 %-zero sparse fp32 (writeZeros, writer.go:407-439), at 256 KiB,
+  1 MiB, 4 MiB and 16 MiB: Writes longer than the window (ring wrap and the cut
+  branch) on the general K1.
+* Len4 literals and Off4 offsets (writer.go:537-597; Decoder reader.go:346-514)
+  from hand-built inputs; the CPU test below checks on the oracle that each
+  input really produces the form it is meant to, so the GPU test cannot pass
+  vacuously.
+
+Bar: every stream's compressed bytes equal the oracle's, byte for byte, and
+every K2 decoder (ring, lane, LDS group, wave, exact) returns the input."""
+
+import numpy as np
+import pytest
+
+import oracle as orc
+
+MiB = 1 << 20
+
+
+def tokens(b: bytes):
+    """Token walk of a compressed stream with the oracle's decoders:
+    [(kind, length, tag bytes, offset bytes, offset field hex)]."""
+    i, out = 0, []
+    while i < len(b):
+        if b[i] == 0:
+            i += 1
+            continue
+        t, l, i2, e = orc.dec_tag(b, i)
+        assert e == 0, (e, i)
+        if t == 0x80 and l == 0:
+            _, ml, i3, e = orc.dec_meta(b, i2)
+            assert e == 0
+            i = i3 + ml
+            continue
+        if t == 0:
+            out.append(("l", l, i2 - i, 0, ""))
+            i = i2 + l
+        else:
+            _, i3, e = orc.dec_offset(b, i2, l)
+            assert e == 0
+            out.append(("c", l, i2 - i, i3 - i2, b[i2:i3].hex()))
+            i = i3
+    return out
+
+
+def long_form_inputs():
+    """(name, bytes, htable, predicate on the oracle's tokens)."""
+    rng = np.random.default_rng(5)
+    r = rng.integers(0, 256, 64, dtype=np.uint8).tobytes()
+    x = rng.integers(0, 256, 70000, dtype=np.uint8).tobytes()
+    return [
+        # a literal of >= 65,916 bytes: Len4 tag (writer.go:555-560)
+        ("len4_literal", x, 1024, lambda t: any(k[0] == "l" and k[1] >= 65916 and k[2] == 5 for k in t)),
+        # a window copy at distance >= 66,044 + l: Off4 (writer.go:590-595)
+        ("off4_window", r + bytes(70000) + r, 1024,
+         lambda t: any(k[0] == "c" and k[3] == 5 and k[4].startswith("fe") for k in t)),
+        # a run-length copy longer than its distance >= 66,044: OffLong + Off4 (writer.go:568-572)
+        ("offlong_off4_run", x + x + x[:5000], 16384,
+         lambda t: any(k[0] == "c" and k[3] == 6 and k[4].startswith("fffe") for k in t)),
+        # a copy longer than 65,916: Len4 copy tag
+        ("len4_copy", x + x + x[:5000], 16384, lambda t: any(k[0] == "c" and k[1] >= 65916 and k[2] == 5 for k in t)),
+    ]
+
+
+def gradient_buckets():
+    """C4 buckets: fp32 N(0,1e-3), bf16 halves, 90 % zeros; 256 KiB .. 16 MiB."""
+    from eazy_amd import synth
+
+    f = synth.f32(41, (16 * MiB) // 4)
+    bf = (synth.f32(43, (4 * MiB) // 2).view(np.uint32) >> 16).astype(np.uint16)
+    sp = synth.f32(47, (4 * MiB) // 4)
+    sp[np.random.default_rng(47).random(sp.shape[0]) < 0.9] = 0.0
+    fb = f.view(np.uint8).tobytes()
+    return [fb[: 256 << 10], fb[: 1 * MiB], fb[: 4 * MiB], bf.view(np.uint8).tobytes(), sp.view(np.uint8).tobytes(), fb]
+
+
+def test_long_form_inputs_produce_their_forms():
+    """CPU: each hand-built input drives the oracle into the token form it names."""
+    for name, b, ht, pred in long_form_inputs():
+        t = tokens(orc.compress(MiB, ht, [b]))
+        assert pred(t), f"{name}: the oracle's stream does not contain the form ({t[:4]})"
+
+
+def _gpu_check(cuda, bufs, htable=1024, kinds=("",)):
+    """Compress on the GPU (K1 kinds as given), byte-compare every stream with
+    the oracle (multi-threaded C oracle), decode with every K2 decoder."""
+    import eazy_amd as ez
+    from test_gpu_batch import _run
+
+    lens = np.array([len(b) for b in bufs], np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    host = np.frombuffer(b"".join(bufs), np.uint8).copy()
+    cap = lens + (lens >> 2) + 64
+    slot_off = np.concatenate([[0], np.cumsum(cap)]).astype(np.int64)
+    slots, sizes = orc.compress_batch(MiB, htable, host, offs, slot_off, 8)
+    want = [slots[slot_off[s] : slot_off[s] + sizes[s]].tobytes() for s in range(len(bufs))]
+    for kind in kinds:
+        ez.select_compress_kernel(kind)
+        try:
+            cb, pk, po, out, osz, ost, _ = _run(cuda, bufs, MiB, htable)
+        finally:
+            ez.select_compress_kernel("")
+        st = cb.status.cpu().numpy()
+        for s, b in enumerate(bufs):
+            assert st[s] == 0, f"K1 {kind!r} stream {s}: compress status {st[s]}"
+            assert pk[po[s] : po[s + 1]].tobytes() == want[s], f"K1 {kind!r} stream {s} (len {len(b)}): bytes differ"
+            assert ost[s] == 0 and osz[s] == len(b), f"stream {s}: decompress status {ost[s]} size {osz[s]}"
+            assert out[offs[s] : offs[s + 1]].tobytes() == b, f"stream {s}: round trip differs"
+    return want
+
+
+@pytest.mark.gpu
+def test_c2_log_writes_256k(cuda):
+    """C2 shape: 32 x 256 KiB log Writes, block 1 MiB, htable 1024 — K1s (T32)
+    and the general K1 forced; K2w is the automatic decoder at this slot size."""
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    assert ez.compress_kernel(MiB, 1024, 256 << 10, 4096) == "s"
+    d = synth.logs(31, 32 * (256 << 10)).tobytes()
+    _gpu_check(cuda, [d[k << 18 : (k + 1) << 18] for k in range(32)], kinds=("", "w"))
+
+
+@pytest.mark.gpu
+def test_c4_gradient_buckets(cuda):
+    """C4 shape: fp32 / bf16 / sparse buckets of 256 KiB .. 16 MiB (Writes up to
+    16x the window: ring wrap, cut, writeZeros, Len4 literals)."""
+    bufs = gradient_buckets()
+    want = _gpu_check(cuda, bufs)
+    t16 = tokens(want[-1])
+    assert any(k[0] == "l" and k[2] == 5 for k in t16), "the 16 MiB fp32 bucket should carry Len4 literals"
+    assert any(k[0] == "c" and k[4] == "ff00" for k in tokens(want[4])), "the sparse bucket should carry zero runs"
+
+
+@pytest.mark.gpu
+def test_long_token_forms(cuda):
+    """Len4 literals / copies, Off4 and OffLong+Off4 offsets, byte-checked on the device."""
+    for name, b, ht, _ in long_form_inputs():
+        _gpu_check(cuda, [b, b[:4096], b], htable=ht)

@@ -244,3 +244,73 @@ def _cmp_oracle(ins, cap, out, sizes, status):
             continue
         assert status[s] == err, s
         assert out[s * cap : s * cap + sizes[s]].tobytes() == want, s
+
+
+def test_writer_cap_too_small_leaves_no_trace(cuda):
+    """ez_writer_write with cap < ez_compress_bound(n) returns EZ_ENOSPC before
+    anything reaches the device; retrying with room gives Go's bytes, and the
+    next Write still matches (the handle's history was not touched)."""
+    import ctypes as C
+
+    import eazy_amd as ez
+    import oracle as orc
+    from eazy_amd import synth
+
+    d = synth.logs(61, 3 * 4096).tobytes()
+    p, q = d[:4096], d[4096:8192]
+    L = ez._lib()
+    h = C.c_void_p()
+    assert L.ez_writer_new(1 << 20, 1024, 0, C.byref(h)) == 0
+    try:
+        n = C.c_size_t()
+        small = (C.c_uint8 * 64)()
+        assert L.ez_writer_write(h, p, len(p), small, 64, C.byref(n)) == ez.ENOSPC and n.value == 0
+        outs = []
+        for x in (p, q):
+            cap = ez.compress_bound(len(x))
+            buf = (C.c_uint8 * cap)()
+            assert L.ez_writer_write(h, x, len(x), buf, cap, C.byref(n)) == 0
+            outs.append(bytes(buf[: n.value]))
+        assert b"".join(outs) == orc.compress(1 << 20, 1024, [p, q])
+    finally:
+        L.ez_writer_free(h)
+
+
+def test_reader_large_stream_small_reads(cuda):
+    """NewReaderBytes over a multi-MiB stream read 4 KiB (and 1000 B) at a time,
+    the shape of io.Copy: the handle uploads input windows from r.i on, not the
+    whole buffer per Read.  Includes a 200 KB literal (longer than the 64 KiB
+    input window) and a NewReader (io.Reader refill) over the same bytes."""
+    import io
+    import time
+
+    import eazy_amd as ez
+    import oracle as orc
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(3)
+    plain = synth.logs(67, 3 << 20).tobytes() + rng.integers(0, 256, 200_000, dtype=np.uint8).tobytes() + \
+        synth.logs(68, 1 << 20).tobytes()
+    comp = orc.compress(1 << 20, 1024, [plain[k : k + 65536] for k in range(0, len(plain), 65536)])
+    for size in (4096, 1000):
+        r = ez.NewReaderBytes(comp)
+        out = bytearray()
+        t0 = time.perf_counter()
+        while True:
+            got, err = r.Read(size)
+            out += got
+            if err == ez.EOF:
+                break
+            assert err == ez.OK, err
+        dt = time.perf_counter() - t0
+        assert bytes(out) == plain, size
+        print(f"Read({size}) loop over {len(comp)} compressed bytes: {dt * 1e3:.0f} ms")
+    r = ez.NewReader(io.BytesIO(comp))
+    out = bytearray()
+    while True:
+        got, err = r.Read(4096)
+        out += got
+        if err == ez.EOF:
+            break
+        assert err == ez.OK, err
+    assert bytes(out) == plain

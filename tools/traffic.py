@@ -10,9 +10,13 @@ import collections
 import csv
 import glob
 import json
+import os
 import sys
 
 root, out = sys.argv[1], sys.argv[2]
+# optional: workload streams stream_bytes -> the summary records the kernel-source hash and shape
+# it was measured at, so bench.py can use it for later runs of the same kernels (profiles/traffic_<w>.json)
+meta = sys.argv[3:6]
 acc = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     per = collections.defaultdict(float)
@@ -30,5 +34,12 @@ for k, v in acc.items():
     fetch = 2.0 * sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"]) if v["FETCH_SIZE"] else None
     write = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"]) if v["WRITE_SIZE"] else None
     res[k] = {"fetch": fetch, "write": write, "traffic": (fetch or 0) + (write or 0) if fetch is not None and write is not None else None}
+if meta:
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+
+    res = {"source_hash": bench.source_hash(), "workload": meta[0], "streams": int(meta[1]),
+           "stream_bytes": int(meta[2]), "kernels": res}
 json.dump(res, open(out, "w"), indent=1)
-print(json.dumps({k: v for k, v in res.items() if k.startswith("k")}, indent=1))
+kern = res.get("kernels", res)
+print(json.dumps({k: v for k, v in kern.items() if k.startswith("k")}, indent=1))
