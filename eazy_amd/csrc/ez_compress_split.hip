@@ -426,6 +426,257 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
     if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
 }
 
+// ---------------------------------------------------------------- K1p, lean single-Write form
+// The same parse as k1_parse<16, true, true, false> (one Write per fresh stream, u16 table,
+// 16 lanes per stream, inputs through L1/L2) with a shorter per-window chain:
+//  * loads need no bounds logic on waves whose streams all have 8 readable bytes before
+//    and 48 after them inside the batch (every wave but the batch's first and last);
+//  * the capped forward count compares real stream bytes and takes min(count, done - cand)
+//    for window matches: below `done` the ring image is the stream, and trim 2
+//    (writer.go:292-296) cuts any window match at w.pos = done, so the zeros the ring holds
+//    from done on never reach a decision or a length;
+//  * the accepting lane computes its own record and the group's next position; the other
+//    lanes take that position with one v_readlane per group (no LDS round trip); the
+//    extra insert of i+1 (writer.go:315-318) is the accepting lane's own second store, after
+//    the visited lanes' one (LDS stores of one wave land in issue order), hashed from its
+//    own bytes x+1 .. x+4;
+//  * only saturated counts (24 forward / 8 backward with room left) take the cooperative
+//    extension (gext), as a rare branch.
+struct GWU {  // unchecked byte view: the caller guarantees [p - 16, p + n + 64) is readable
+    const uint8_t *p;
+    __device__ __forceinline__ V16 at(int32_t y) const { return ld16v(p + (y - 8)); }  // bytes y-8 .. y+7
+    // GW::around without the batch-bounds branch (gext's view): bytes before the stream read 0
+    __device__ __forceinline__ void around(int32_t y, uint64_t &before, uint64_t &from) const {
+        V16 v = at(y);
+        if (y < 8) {
+            const int32_t k = 8 - y;
+            v.lo &= k >= 8 ? 0ull : ~0ull << (8 * k);
+            v.hi &= k >= 16 ? 0ull : (k <= 8 ? ~0ull : ~0ull << (8 * (k - 8)));
+        }
+        before = v.lo;
+        from = v.hi;
+    }
+    __device__ __forceinline__ uint32_t u32(int32_t y) const { return *(const uint32_t __attribute__((aligned(1))) *)(p + y); }
+};
+struct GWC : GW {  // checked view with the lean loop's at()
+    __device__ __forceinline__ V16 at(int32_t y) const {
+        V16 v;
+        around(y, v.lo, v.hi);
+        return v;
+    }
+};
+
+// The window's bytes of a group by one coalesced dword per lane: lane k of the group loads
+// dword k of the 64-byte region from floor4(p + i - 8), and every lane assembles its 32 bytes
+// (x-8 .. x+23) from 9 of those dwords with ds_bpermute + v_alignbyte.  One global load of 64 lanes
+// touching ~4 cache lines, instead of two 16-byte loads per lane at 64 overlapping unaligned
+// addresses: the parse is bound by the vector-memory path's per-lane cache accesses (TA/TD ~90 %
+// busy, ~2 accesses per lane per load), not by HBM.
+struct WinDw {
+    uint32_t dw, r0;  // this lane's dword of the region; the region's start offset (0..3) from p + i - 8
+    __device__ __forceinline__ void load(const uint8_t *p, int32_t i, int lj) {
+        const uintptr_t a = (uintptr_t)(p + i - 8);
+        r0 = (uint32_t)(a & 3);
+        dw = *(const uint32_t *)((a & ~(uintptr_t)3) + 4 * (uint32_t)lj);
+    }
+    __device__ __forceinline__ void bytes(int g, int lj, V16 &w0, V16 &w1) const {
+        const uint32_t o = (uint32_t)lj + r0, q = o >> 2, r = o & 3;
+        const int src = 4 * (16 * g + (int)q);
+        uint32_t d[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) d[t] = (uint32_t)__builtin_amdgcn_ds_bpermute(src + 4 * t, (int)dw);
+        uint32_t b[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+        w0.lo = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+        w0.hi = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
+        w1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
+        w1.hi = (uint64_t)b[6] | ((uint64_t)b[7] << 32);
+    }
+};
+
+template <class SRC>
+__device__ __forceinline__ void lean_loop(const SRC &P, int32_t n, int lj, int g, uint16_t *hth, uint32_t hsh, uint64_t *rec, uint64_t rcap,
+                                          int prio, int32_t &nrec_out, int &err) {
+    constexpr int G = 16;
+    constexpr bool DW = std::is_same<SRC, GWU>::value;  // window bytes by dwords (interior waves)
+    int32_t i = 0, done = 0, nrec = 0;
+    bool live = !err && n >= 4;
+    int32_t guard = 4 * n + 64;
+    V16 w0{0, 0}, w1{0, 0};  // bytes x-8 .. x+7 and x+8 .. x+23 of this lane's position x
+    WinDw wd{0, 0};
+    // the bytes around stream position 0, the candidate of every zero table entry:
+    // judged without a load
+    V16 z0{0, 0}, z1{0, 0};
+    if (live) {
+        z0 = P.at(0);
+        z1 = P.at(16);
+        z0.lo = 0;
+    }
+    if (DW) {
+        wd.load(P.p, 0, lj);
+    } else if (live) {
+        w0 = P.at(lj);
+        w1 = P.at(lj + 16);
+    }
+    while (__ballot(live) != 0) {
+        if (DW) wd.bytes(g, lj, w0, w1);
+        if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
+        const int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
+        const int32_t x = i + lj;
+        const bool valid = live && lj < nvalid;
+
+        // ---- visit (writer.go:213-217): hash, table, nearest earlier lane with the same hash
+        if (prio & 1) __builtin_amdgcn_s_setprio(3);
+        const uint32_t h = valid ? ((uint32_t)w0.hi * kHashMul) >> hsh : 0u;
+        const int32_t tv = valid ? (int32_t)hth[h] : 0;
+        const int32_t d = Pred<G - 1, true>::get(h, lj, 0);
+        const int32_t cand = valid ? (d ? x - d : tv) : 0;
+        V16 c0 = z0, c1 = z1;
+        if (cand != 0) {
+            c0 = P.at(cand);
+            c1 = P.at(cand + 16);
+            // bytes before the stream start are the fresh ring's zeros
+            c0.lo &= cand >= 8 ? ~0ull : ~0ull << (8 * (8 - cand));
+        }
+        if (prio & 1) __builtin_amdgcn_s_setprio(0);
+
+        // ---- capped judgement, writer.go:219-301 (window) and :441-463 (writeRunlen)
+        const bool rl = cand >= done && cand < x;
+        const uint64_t e0 = w0.hi ^ c0.hi, e1 = w1.lo ^ c1.lo, e2 = w1.hi ^ c1.hi;
+        int32_t jf = e0 ? ctz_bytes(e0) : (e1 ? 8 + ctz_bytes(e1) : 16 + ctz_bytes(e2));
+        jf = jf < n - x ? jf : n - x;
+        int32_t bl = x - done;
+        if (rl) bl = bl < cand ? bl : cand;
+        int32_t jb = clz_bytes(w0.lo ^ c0.lo);
+        jb = jb < bl ? jb : bl;
+        const bool zr = rl && c0.hi == 0 && cand + 8 < n;
+        const int32_t fw = rl ? jf : (jf < done - cand ? jf : done - cand);
+        const bool acc = valid && (zr || fw + jb >= kMinCopyChunk);
+
+        // ---- this lane's action if it is the group's first acceptor
+        int32_t lit, nx, dist, ext;
+        bool force = false;
+        if (zr) {  // writeZeros :407-439
+            int32_t zf = 8 + (c1.lo ? ctz_bytes(c1.lo) : 8 + ctz_bytes(c1.hi));
+            zf = zf < n - cand ? zf : n - cand;
+            int32_t zb = clz_bytes(c0.lo);
+            zb = zb < cand - done ? zb : cand - done;
+            lit = cand - zb;
+            nx = cand + zf;
+            dist = 0;
+            ext = (zf == 24 && n - cand > 24 ? 1 : 0) | (zb == 8 && cand - done > 8 ? 2 : 0);
+        } else {  // writeRunlen :441-489 / window match :303-321
+            lit = x - jb;
+            nx = x + fw;
+            dist = x - cand;
+            force = rl;
+            ext = (jf == 24 && (rl ? n - x : (done - cand < n - x ? done - cand : n - x)) > 24 ? 1 : 0) | (jb == 8 && bl > 8 ? 2 : 0);
+        }
+        const uint64_t am64 = __ballot(acc);
+        const uint32_t am = (uint32_t)(am64 >> (G * g)) & 0xffffu;
+        const int a = am ? __builtin_ctz(am) : -1;
+        const bool act = live && a >= 0;
+        // the group's next position (and whether the acceptor needs an exact extension), one
+        // v_readlane per group
+        const int32_t pack = nx | (ext << 28);
+        int32_t sel = 0;
+#pragma unroll
+        for (int gg = 0; gg < 64 / G; gg++) {
+            const uint32_t m = (uint32_t)(am64 >> (G * gg)) & 0xffffu;
+            const int32_t v = __builtin_amdgcn_readlane(pack, G * gg + (m ? __builtin_ctz(m) : 0));
+            sel = g == gg ? v : sel;
+        }
+        int32_t nxt = sel & 0x0fffffff;
+        if (__ballot(act && (sel >> 28) != 0) != 0) {
+            // rare: a saturated count; exact lengths by the whole group (as k1_parse)
+            // the acceptor's candidate, capped backward count (<= 8) and branch
+            const int32_t info = cand | (((zr ? cand : x) - lit) << 16) | ((int32_t)rl << 29) | ((int32_t)zr << 30);
+            const int32_t ib = bcast(info, G * g + (a < 0 ? 0 : a));
+            const int32_t xa = i + (a < 0 ? 0 : a);
+            const int32_t ca = ib & 0xffff;
+            const bool rla = (ib >> 29) & 1, zra = (ib >> 30) & 1;
+            const int32_t e = (sel >> 28) & 3;
+            const bool need = act && e != 0;
+            const int mode = zra ? 0 : (rla ? 1 : 2);
+            const int32_t fa = zra ? ca : xa;
+            const int32_t blim = zra ? ca - done : (rla ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
+            const int32_t flim = zra ? n - ca : (rla ? n - xa : ((done - ca) < n - xa ? done - ca : n - xa));
+            int32_t fx, cx;
+            gext<G, SRC>(P, need && (e & 1), need && (e & 2), g, lj, fa, ca, mode, done, 24, flim, blim, fx, cx);
+            if (need) {
+                const int32_t f = (e & 1) ? fx : (sel & 0x0fffffff) - fa;
+                const int32_t c = (e & 2) ? cx : ((ib >> 16) & 0xf);
+                nxt = fa + f;
+                if (lj == a) {
+                    lit = fa - c;
+                    nx = nxt;
+                }
+            }
+        }
+        // ---- table: the visited lanes' positions (the last of a hash wins), then lane a's i+1
+        if (valid && (a < 0 || lj <= a)) hth[h] = (uint16_t)x;
+        if (act && lj == a) {
+            if (!rl && !zr && x + 1 + 4 <= n) hth[((uint32_t)(w0.hi >> 8) * kHashMul) >> hsh] = (uint16_t)(x + 1);
+            if ((uint64_t)nrec < rcap) __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), rec + nrec);
+        }
+        if (act) {
+            if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
+            nrec++;
+            i = done = nxt;
+        } else if (live) {
+            i += nvalid;
+        }
+        if (live && (err || i + 4 > n)) live = false;
+        // the next window's bytes
+        if (DW) {
+            wd.load(P.p, live ? i : 0, lj);
+        } else if (live) {
+            w0 = P.at(i + lj);
+            w1 = P.at(i + lj + 16);
+        }
+    }
+    nrec_out = nrec;
+}
+
+__global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
+                                                 uint64_t rcap, int prio) {
+    constexpr int G = 16, S = 64 / G;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = (int)(threadIdx.x & 63);
+    const int g = lane / G, lj = lane % G;
+    const int32_t hs = (int32_t)A.hs;
+    const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(hs - 1)));
+    uint16_t *hth = (uint16_t *)((uint32_t *)smem + (uint32_t)g * stride_words);
+    const uint64_t s = (uint64_t)blockIdx.x * S + g;
+    const bool have = s < A.count;
+    int32_t n = 0;
+    const uint8_t *gp = A.in;
+    const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
+    if (have) {
+        n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+        gp = A.in + A.in_off[s];
+    }
+    for (int32_t k = 4 * lj; k < (int32_t)table_words; k += 4 * G) *(uint4 *)((uint32_t *)hth + k) = make_uint4(0, 0, 0, 0);
+    // the launcher sized records and tables from max_len: longer streams are refused; a lane
+    // group without a stream never enters the loop
+    int err = !have || (uint64_t)n > A.max_len ? EZ_EINVAL : 0;
+    uint64_t *rec = recs + (have ? s * rcap : 0);
+    const bool safe = have && gp - 16 >= blo && gp + n + 64 <= bhi;
+    int32_t nrec = 0;
+    if (__ballot(!safe) == 0) {
+        GWU P{gp};
+        lean_loop(P, n, lj, g, hth, hsh, rec, rcap, prio, nrec, err);
+    } else {
+        GWC P;
+        P.p = gp;
+        P.blo = blo;
+        P.bhi = bhi;
+        lean_loop(P, n, lj, g, hth, hsh, rec, rcap, prio, nrec, err);
+    }
+    if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
+}
+
 // ---------------------------------------------------------------- K1e
 // 16 bytes at y of the batch [lo, hi) (bytes outside read as 0)
 __device__ __forceinline__ V16 ld16_in(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
@@ -629,6 +880,30 @@ hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st)
     return hipGetLastError();
 }
 
+// the lean single-Write parse (k1_lean) + the token writer; EZ_K1S_LEAN=0 takes k1_parse (A/B)
+bool split_lean() {
+    static const bool v = !(getenv("EZ_K1S_LEAN") && atoi(getenv("EZ_K1S_LEAN")) == 0);
+    return v;
+}
+hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void *)k1_lean, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_done = true;
+    }
+    constexpr int S = 4;
+    const uint32_t stride = split_stride<16, true, true>(a), tw = split_table_words<true>(a);
+    const uint64_t rcap = rec_cap(a);
+    const unsigned grid = (unsigned)((a.count + S - 1) / S);
+    static const int prio = getenv("EZ_K1S_PRIO") ? atoi(getenv("EZ_K1S_PRIO")) : 1;
+    hipLaunchKernelGGL(k1_lean, dim3(grid), dim3(64), (size_t)stride * 4 * S, st, a, stride, tw, recs, rcap, prio);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    const unsigned egrid = (unsigned)((a.count + 3) / 4);
+    hipLaunchKernelGGL(k1_emit, dim3(egrid), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
+    return hipGetLastError();
+}
+
 // The property T16 relies on, checked once per process on the device:
 // same-address ds_write_b16 of one wave instruction land in ascending lane
 // order (the highest lane's value stays).
@@ -693,6 +968,7 @@ hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipSt
     // EZ_K1S_GIN=0 (experiments): inputs staged in LDS when they fit
     const bool lds_in = !split_gin() && (G == 8 ? split_stride<8, true, false>(a) : split_stride<16, true, false>(a)) != 0;
     if (T == 16 && lds_in) return G == 8 ? launch_split_g<8, true, false, false>(a, recs, st) : launch_split_g<16, true, false, false>(a, recs, st);
+    if (T == 16 && G == 16 && split_lean()) return launch_lean(a, recs, st);
     if (T == 16) return G == 8 ? launch_split_g<8, true, true, false>(a, recs, st) : launch_split_g<16, true, true, false>(a, recs, st);
     if (split_g32(a.count) == 32) return launch_split_g<32, false, true, false>(a, recs, st);
     return G == 8 ? launch_split_g<8, false, true, false>(a, recs, st) : launch_split_g<16, false, true, false>(a, recs, st);

@@ -1,0 +1,78 @@
+"""Per-Write latency of the streaming drop-in (one long-lived Writer handle,
+ez_writer_write through the C-ABI) for the reference's benchmark shape: many
+small Writes of log events on one Writer (eazy_test.go:1156-1193), next to the
+C oracle's Writer on one host thread.  Also a Reader.Read loop over the result.
+Prints one JSON line.  Usage: python tests/perf_handle.py [--writes K]"""
+
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
+
+import numpy as np  # noqa: E402
+
+import eazy_amd as ez  # noqa: E402
+import oracle as orc  # noqa: E402
+from eazy_amd import synth  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--writes", type=int, default=2000)
+    a = ap.parse_args()
+    L = ez._lib()
+    src = synth.logs(91, 64 << 20).tobytes()
+    res = {}
+    for size in (100, 400, 1024, 4096):
+        ws = [src[k * size : (k + 1) * size] for k in range(a.writes)]
+        h = C.c_void_p()
+        assert L.ez_writer_new(1 << 20, 1024, 0, C.byref(h)) == 0
+        cap = ez.compress_bound(size)
+        buf = (C.c_uint8 * cap)()
+        n = C.c_size_t()
+        outs = []
+        for w in ws[:20]:  # warm-up on a throwaway stream
+            assert L.ez_writer_write(h, w, size, buf, cap, C.byref(n)) == 0
+        assert L.ez_writer_reset(h) == 0
+        lat = []
+        for w in ws:
+            t0 = time.perf_counter()
+            assert L.ez_writer_write(h, w, size, buf, cap, C.byref(n)) == 0
+            lat.append(time.perf_counter() - t0)
+            outs.append(bytes(buf[: n.value]))
+        L.ez_writer_free(h)
+        gpu = b"".join(outs)
+        ow = orc.Writer(1 << 20, 1024)
+        t0 = time.perf_counter()
+        for w in ws:
+            ow.write(w)
+        t_cpu = (time.perf_counter() - t0) / len(ws)
+        assert gpu == ow.sink, f"size {size}: handle bytes differ from the oracle"
+        lat = np.array(lat) * 1e6
+        res[str(size)] = {"gpu_us_p50": float(np.median(lat)), "gpu_us_p99": float(np.percentile(lat, 99)),
+                          "gpu_MiBps": size / (lat.mean() / 1e6) / 2**20,
+                          "cpu_oracle_us": t_cpu * 1e6, "cpu_oracle_MiBps": size / t_cpu / 2**20}
+        # Reader.Read(4 KiB) loop over the stream
+        r = ez.NewReaderBytes(gpu)
+        got = bytearray()
+        t0 = time.perf_counter()
+        while True:
+            d, err = r.Read(4096)
+            got += d
+            if err == ez.EOF:
+                break
+            assert err == ez.OK
+        t_r = time.perf_counter() - t0
+        assert bytes(got) == b"".join(ws)
+        res[str(size)]["reader_4k_MiBps"] = len(got) / t_r / 2**20
+    print(json.dumps({"handle_path": res, "writes_per_size": a.writes,
+                      "note": "ez_writer_write per call: H2D copy, one wave-per-stream kernel, D2H copy, sync"}))
+
+
+if __name__ == "__main__":
+    main()
