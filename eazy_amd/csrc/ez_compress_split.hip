@@ -442,12 +442,19 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
 //    own bytes x+1 .. x+4;
 //  * only saturated counts (24 forward / 8 backward with room left) take the cooperative
 //    extension (gext), as a rare branch.
-struct GWU {  // unchecked byte view: the caller guarantees [p - 16, p + n + 64) is readable
+// Loads of the lean parse carry no bounds logic: every stream the loop reads has 16 readable bytes
+// before it and 64 after it (k1_lean copies the few streams at the batch's edges into padded
+// slots first), so each piece is one plain aligned load.
+struct LeanIn {
+    __device__ __forceinline__ uint32_t dw(const uint8_t *w) const { return *(const uint32_t *)w; }
+    __device__ __forceinline__ uint4 dw4(const uint8_t *w) const { return *(const uint4 *)w; }
+};
+// gext's view of a padded stream: GW::around without the batch-bounds branch (bytes before the
+// stream start read 0; gext reads at most 16 bytes before it and 16 after its end)
+struct GWU {
     const uint8_t *p;
-    __device__ __forceinline__ V16 at(int32_t y) const { return ld16v(p + (y - 8)); }  // bytes y-8 .. y+7
-    // GW::around without the batch-bounds branch (gext's view): bytes before the stream read 0
     __device__ __forceinline__ void around(int32_t y, uint64_t &before, uint64_t &from) const {
-        V16 v = at(y);
+        V16 v = ld16v(p + (y - 8));
         if (y < 8) {
             const int32_t k = 8 - y;
             v.lo &= k >= 8 ? 0ull : ~0ull << (8 * k);
@@ -456,28 +463,20 @@ struct GWU {  // unchecked byte view: the caller guarantees [p - 16, p + n + 64)
         before = v.lo;
         from = v.hi;
     }
-    __device__ __forceinline__ uint32_t u32(int32_t y) const { return *(const uint32_t __attribute__((aligned(1))) *)(p + y); }
-};
-struct GWC : GW {  // checked view with the lean loop's at()
-    __device__ __forceinline__ V16 at(int32_t y) const {
-        V16 v;
-        around(y, v.lo, v.hi);
-        return v;
-    }
 };
 
 // The window's bytes of a group by one coalesced dword per lane: lane k of the group loads
 // dword k of the 64-byte region from floor4(p + i - 8), and every lane assembles its 32 bytes
 // (x-8 .. x+23) from 9 of those dwords with ds_bpermute + v_alignbyte.  One global load of 64 lanes
 // touching ~4 cache lines, instead of two 16-byte loads per lane at 64 overlapping unaligned
-// addresses: the parse is bound by the vector-memory path's per-lane cache accesses (TA/TD ~90 %
-// busy, ~2 accesses per lane per load), not by HBM.
+// addresses: the parse is bound by the vector-memory path's per-lane L1 accesses (TA/TD ~90 % busy
+// at two byte-unaligned 16-byte loads per lane and window), not by HBM.
 struct WinDw {
     uint32_t dw, r0;  // this lane's dword of the region; the region's start offset (0..3) from p + i - 8
-    __device__ __forceinline__ void load(const uint8_t *p, int32_t i, int lj) {
+    __device__ __forceinline__ void load(const LeanIn &L, const uint8_t *p, int32_t i, int lj) {
         const uintptr_t a = (uintptr_t)(p + i - 8);
         r0 = (uint32_t)(a & 3);
-        dw = *(const uint32_t *)((a & ~(uintptr_t)3) + 4 * (uint32_t)lj);
+        dw = L.dw((const uint8_t *)((a & ~(uintptr_t)3) + 4 * (uint32_t)lj));
     }
     __device__ __forceinline__ void bytes(int g, int lj, V16 &w0, V16 &w1) const {
         const uint32_t o = (uint32_t)lj + r0, q = o >> 2, r = o & 3;
@@ -495,11 +494,29 @@ struct WinDw {
     }
 };
 
-template <class SRC>
-__device__ __forceinline__ void lean_loop(const SRC &P, int32_t n, int lj, int g, uint16_t *hth, uint32_t hsh, uint64_t *rec, uint64_t rcap,
-                                          int prio, int32_t &nrec_out, int &err) {
+// The 32 bytes y-8 .. y+23 by dword-aligned loads (dwordx4, dwordx4, dword from floor4(p + y - 8))
+// and v_alignbyte: a 16-byte load at a byte-unaligned address costs the L1 one access per dword it
+// touches, an aligned one a single access (tools/mb_ta.hip, L1-resident: 64 vs 16 ns per scattered
+// wave-load), so this is 3 accesses per lane instead of ~8.
+__device__ __forceinline__ void bytes32(const LeanIn &L, const uint8_t *p, int32_t y, V16 &c0, V16 &c1) {
+    const uintptr_t a = (uintptr_t)(p + y - 8);
+    const uint32_t r = (uint32_t)(a & 3);
+    const uint8_t *w = (const uint8_t *)(a & ~(uintptr_t)3);
+    const uint4 q0 = L.dw4(w), q1 = L.dw4(w + 16);
+    const uint32_t q2 = L.dw(w + 32);
+    const uint32_t d[9] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2};
+    uint32_t b[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+    c0.lo = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+    c0.hi = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
+    c1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
+    c1.hi = (uint64_t)b[6] | ((uint64_t)b[7] << 32);
+}
+
+__device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int32_t n, int lj, int g, uint16_t *hth,
+                                          uint32_t hsh, uint64_t *rec, uint64_t rcap, int prio, int32_t &nrec_out, int &err) {
     constexpr int G = 16;
-    constexpr bool DW = std::is_same<SRC, GWU>::value;  // window bytes by dwords (interior waves)
     int32_t i = 0, done = 0, nrec = 0;
     bool live = !err && n >= 4;
     int32_t guard = 4 * n + 64;
@@ -509,18 +526,12 @@ __device__ __forceinline__ void lean_loop(const SRC &P, int32_t n, int lj, int g
     // judged without a load
     V16 z0{0, 0}, z1{0, 0};
     if (live) {
-        z0 = P.at(0);
-        z1 = P.at(16);
+        bytes32(L, p, 0, z0, z1);
         z0.lo = 0;
     }
-    if (DW) {
-        wd.load(P.p, 0, lj);
-    } else if (live) {
-        w0 = P.at(lj);
-        w1 = P.at(lj + 16);
-    }
+    wd.load(L, p, 0, lj);
     while (__ballot(live) != 0) {
-        if (DW) wd.bytes(g, lj, w0, w1);
+        wd.bytes(g, lj, w0, w1);
         if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
         const int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
         const int32_t x = i + lj;
@@ -534,8 +545,7 @@ __device__ __forceinline__ void lean_loop(const SRC &P, int32_t n, int lj, int g
         const int32_t cand = valid ? (d ? x - d : tv) : 0;
         V16 c0 = z0, c1 = z1;
         if (cand != 0) {
-            c0 = P.at(cand);
-            c1 = P.at(cand + 16);
+            bytes32(L, p, cand, c0, c1);
             // bytes before the stream start are the fresh ring's zeros
             c0.lo &= cand >= 8 ? ~0ull : ~0ull << (8 * (8 - cand));
         }
@@ -603,7 +613,7 @@ __device__ __forceinline__ void lean_loop(const SRC &P, int32_t n, int lj, int g
             const int32_t blim = zra ? ca - done : (rla ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
             const int32_t flim = zra ? n - ca : (rla ? n - xa : ((done - ca) < n - xa ? done - ca : n - xa));
             int32_t fx, cx;
-            gext<G, SRC>(P, need && (e & 1), need && (e & 2), g, lj, fa, ca, mode, done, 24, flim, blim, fx, cx);
+            gext<G, GWU>(GWU{p}, need && (e & 1), need && (e & 2), g, lj, fa, ca, mode, done, 24, flim, blim, fx, cx);
             if (need) {
                 const int32_t f = (e & 1) ? fx : (sel & 0x0fffffff) - fa;
                 const int32_t c = (e & 2) ? cx : ((ib >> 16) & 0xf);
@@ -628,19 +638,22 @@ __device__ __forceinline__ void lean_loop(const SRC &P, int32_t n, int lj, int g
             i += nvalid;
         }
         if (live && (err || i + 4 > n)) live = false;
-        // the next window's bytes
-        if (DW) {
-            wd.load(P.p, live ? i : 0, lj);
-        } else if (live) {
-            w0 = P.at(i + lj);
-            w1 = P.at(i + lj + 16);
-        }
+        wd.load(L, p, live ? i : 0, lj);  // the next window's bytes
     }
     nrec_out = nrec;
 }
 
+// Edge slots (after the records in the K1 scratch): a zeroed 128-byte dummy region for lane groups
+// without a stream, then kEdgeSlots slots of edge_slot_bytes, then the slot counter (zeroed by the
+// launcher).  A live stream (n >= 4) lacks the 16 bytes before or the 64 after it only if it starts
+// in the batch's first 16 bytes (at most 4 such streams, each >= 4 bytes) or ends in its last 64
+// (at most 16): 20 slots always suffice.
+constexpr int kEdgeSlots = 24;
+__host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + 16 + 64 + 15) & ~15ull; }
+__host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs &a) { return 128 + kEdgeSlots * edge_slot_bytes(a) + 16; }
+
 __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
-                                                 uint64_t rcap, int prio) {
+                                                 uint64_t rcap, int prio, uint8_t *edge) {
     constexpr int G = 16, S = 64 / G;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = (int)(threadIdx.x & 63);
@@ -650,30 +663,36 @@ __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride
     uint16_t *hth = (uint16_t *)((uint32_t *)smem + (uint32_t)g * stride_words);
     const uint64_t s = (uint64_t)blockIdx.x * S + g;
     const bool have = s < A.count;
-    int32_t n = 0;
-    const uint8_t *gp = A.in;
     const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
+    int32_t n = 0;
+    const uint8_t *src = blo;
     if (have) {
         n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
-        gp = A.in + A.in_off[s];
+        src = A.in + A.in_off[s];
     }
     for (int32_t k = 4 * lj; k < (int32_t)table_words; k += 4 * G) *(uint4 *)((uint32_t *)hth + k) = make_uint4(0, 0, 0, 0);
     // the launcher sized records and tables from max_len: longer streams are refused; a lane
-    // group without a stream never enters the loop
+    // group without a live stream never enters the loop and reads only the dummy region
     int err = !have || (uint64_t)n > A.max_len ? EZ_EINVAL : 0;
+    const bool live = !err && n >= 4;
     uint64_t *rec = recs + (have ? s * rcap : 0);
-    const bool safe = have && gp - 16 >= blo && gp + n + 64 <= bhi;
-    int32_t nrec = 0;
-    if (__ballot(!safe) == 0) {
-        GWU P{gp};
-        lean_loop(P, n, lj, g, hth, hsh, rec, rcap, prio, nrec, err);
-    } else {
-        GWC P;
-        P.p = gp;
-        P.blo = blo;
-        P.bhi = bhi;
-        lean_loop(P, n, lj, g, hth, hsh, rec, rcap, prio, nrec, err);
+    const uint8_t *p = live ? src : edge + 16;
+    const bool edge_stream = live && (src - 16 < blo || src + n + 64 > bhi);
+    if (__ballot(edge_stream) != 0) {
+        // copy each edge stream of the wave into a slot: [16 zero bytes][the stream][64 zero bytes]
+        int32_t slot = 0;
+        if (edge_stream && lj == 0) slot = (int32_t)atomicAdd((uint32_t *)(edge + 128 + kEdgeSlots * edge_slot_bytes(A)), 1u);
+        slot = bcast(slot, G * g);
+        if (edge_stream && slot >= kEdgeSlots) err = EZ_ESTUCK;  // cannot happen (20 slots suffice)
+        if (edge_stream && !err) {
+            uint8_t *d = edge + 128 + (uint64_t)slot * edge_slot_bytes(A);
+            for (int32_t k = lj; k < n + 80; k += G) d[k] = (k >= 16 && k < n + 16) ? src[k - 16] : (uint8_t)0;
+            p = d + 16;
+        }
+        __threadfence_block();
     }
+    int32_t nrec = 0;
+    lean_loop(LeanIn{}, p, n, lj, g, hth, hsh, rec, rcap, prio, nrec, err);
     if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
 }
 
@@ -896,7 +915,11 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     const uint64_t rcap = rec_cap(a);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     static const int prio = getenv("EZ_K1S_PRIO") ? atoi(getenv("EZ_K1S_PRIO")) : 1;
-    hipLaunchKernelGGL(k1_lean, dim3(grid), dim3(64), (size_t)stride * 4 * S, st, a, stride, tw, recs, rcap, prio);
+    uint8_t *edge = (uint8_t *)(recs + a.count * rcap);
+    hipError_t z = hipMemsetAsync(edge, 0, 128, st);
+    if (z == hipSuccess) z = hipMemsetAsync(edge + 128 + kEdgeSlots * edge_slot_bytes(a), 0, 16, st);
+    if (z != hipSuccess) return z;
+    hipLaunchKernelGGL(k1_lean, dim3(grid), dim3(64), (size_t)stride * 4 * S, st, a, stride, tw, recs, rcap, prio, edge);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
@@ -955,7 +978,8 @@ void select_split_table(bool t32) { g_split_t32 = t32; }
 
 uint32_t split_stride_words(const CompressArgs &a) { return split_table(a) != 0 ? 1u : 0u; }
 
-uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a) * 2; }
+// records (8 bytes per record slot entry), then k1_lean's edge area
+uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a) * 2 + (edge_area_bytes(a) + 3) / 4; }
 
 hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t st) {
     uint64_t *recs = (uint64_t *)scratch;

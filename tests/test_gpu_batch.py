@@ -256,3 +256,19 @@ def test_sub_batches_through_offset_views(cuda):
     assert torch.equal(torch.cat(got), want), "chunked packing differs from the one-batch packing"
     assert torch.equal(osz.cpu(), torch.from_numpy(lens.astype(np.int64)))
     assert out[: int(offs[-1])].cpu().numpy().tobytes() == host.tobytes()
+
+
+def test_batch_edge_streams(cuda, k1_kind):
+    """Streams at the batch's edges (the lean parse copies a live stream that lacks 16 readable
+    bytes before it or 64 after it inside the batch into a padded slot): many empty streams, then
+    live ones starting at offset 0..12; tiny live streams ending in the last 64 bytes; a batch
+    shorter than 16 bytes; single-stream batches."""
+    from eazy_amd import synth
+
+    d = synth.logs(29, 1 << 16).tobytes()
+    head = [b""] * 37 + [d[:4], d[4:9], d[9:14], d[14:600]]
+    tail = [d[600:4600]] + [d[4600 + 5 * k : 4605 + 5 * k] for k in range(14)] + [d[4700:4704]]
+    _check(cuda, head + [d[5000:9000]] * 9 + tail)
+    _check(cuda, [b"abcabcabcab"])
+    _check(cuda, [d[:4096]])
+    _check(cuda, [b"", d[:6000], b""])

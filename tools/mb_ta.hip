@@ -26,8 +26,10 @@ __device__ __forceinline__ uint32_t rnd(uint32_t &s) {
 }
 
 template <int P>
-__global__ __launch_bounds__(64) void k(const uint8_t *buf, uint32_t mask, int iters, uint32_t *out) {
+__global__ __launch_bounds__(64) void k(const uint8_t *buf0, uint32_t mask, int iters, uint32_t *out) {
     const uint32_t lane = threadIdx.x;
+    // L1 mode (mask < 64 KiB): every CU's waves share one small region (L1-resident after the first pass)
+    const uint8_t *buf = mask < 65536 ? buf0 + (size_t)(blockIdx.x % 256) * 65536 : buf0;
     uint32_t s = 0x9e3779b9u * (blockIdx.x * 64 + lane + 1);
     uint32_t acc = 0;
     for (int it = 0; it < iters; it++) {
@@ -66,7 +68,7 @@ float run(const uint8_t *buf, uint32_t mask, int iters, uint32_t *out, int block
 
 int main(int argc, char **argv) {
     const int iters = argc > 1 ? atoi(argv[1]) : 2000;
-    const size_t bytes = 8u << 20;  // L2-resident per XCD after the first touch: 8 MiB spread over 8 XCDs
+    const size_t bytes = 16u << 20;  // L2-resident per XCD after the first touch: 8 MiB spread over 8 XCDs
     uint8_t *buf;
     uint32_t *out;
     hipMalloc(&buf, bytes + 64);
@@ -77,18 +79,22 @@ int main(int argc, char **argv) {
                            "coalesced dword", "scatter dwordx2 byte-aligned", "scatter dword byte-aligned",
                            "scatter dwordx4 4B-aligned", "coalesced dwordx4"};
     float t[8];
-    t[0] = run<0>(buf, (uint32_t)(bytes - 1), iters, out, blocks);
-    t[1] = run<1>(buf, (uint32_t)(bytes - 1), iters, out, blocks);
-    t[2] = run<2>(buf, (uint32_t)(bytes - 1), iters, out, blocks);
-    t[3] = run<3>(buf, (uint32_t)(bytes - 1), iters, out, blocks);
-    t[4] = run<4>(buf, (uint32_t)(bytes - 1), iters, out, blocks);
-    t[5] = run<5>(buf, (uint32_t)(bytes - 1), iters, out, blocks);
-    t[6] = run<6>(buf, (uint32_t)(bytes - 1), iters, out, blocks);
-    t[7] = run<7>(buf, (uint32_t)(bytes - 1), iters, out, blocks);
+    for (int mode = 0; mode < 2; mode++) {
+    const uint32_t m = mode == 0 ? (uint32_t)(bytes - 1) : 16383u;  // 8 MiB (L2) or 16 KiB per CU (L1)
+    printf(mode == 0 ? "-- 8 MiB buffer (L1 misses, L2 hits)\n" : "-- 16 KiB per CU (L1 hits)\n");
+    t[0] = run<0>(buf, m, iters, out, blocks);
+    t[1] = run<1>(buf, m, iters, out, blocks);
+    t[2] = run<2>(buf, m, iters, out, blocks);
+    t[3] = run<3>(buf, m, iters, out, blocks);
+    t[4] = run<4>(buf, m, iters, out, blocks);
+    t[5] = run<5>(buf, m, iters, out, blocks);
+    t[6] = run<6>(buf, m, iters, out, blocks);
+    t[7] = run<7>(buf, m, iters, out, blocks);
     for (int p = 0; p < 8; p++) {
         const double loads_per_cu = (double)blocks / 256 * iters * 4;
         printf("%d %-32s %8.3f ms  %7.1f wave-loads/CU/us  %6.1f ns per wave-load per CU\n", p, names[p], t[p],
                loads_per_cu / (t[p] * 1e3), t[p] * 1e6 / loads_per_cu);
+    }
     }
     return 0;
 }
