@@ -130,7 +130,7 @@ def device_count() -> int:
 
 def compress_kernel(block: int, htable: int, max_len: int, count: int) -> str:
     """The K1 kernel a batch of `count` fresh streams of <= max_len bytes runs
-    on the current device ('t' tile, 'r' grp, 'l' lane, ...)."""
+    on the current device ('s' K1s: parse + token writer, 'w' general wave per stream)."""
     L = _lib()
     L.ez_compress_kernel.argtypes = [C.c_int64, C.c_int64, C.c_uint64, C.c_uint64]
     v = L.ez_compress_kernel(block, htable, max_len, count)
@@ -140,13 +140,13 @@ def compress_kernel(block: int, htable: int, max_len: int, count: int) -> str:
 
 
 def select_compress_kernel(kind: str = "") -> None:
-    """Force the K1 kernel of later batch calls ('s', 'S', 't', ...; '' =
-    automatic).  Tests and A/B measurement only."""
+    """Force the K1 kernel of later batch calls ('s' K1s, 'S' K1s with the u32
+    exchange table, 'w' general; '' = automatic).  Tests and A/B measurement only."""
     _check(_lib().ez_select_compress_kernel(ord(kind) if kind else 0))
 
 
 def select_decompress_kernel(kind: str = "") -> None:
-    """Force the first K2 kernel of later batch decodes ('r', 'f', 'g', 'w';
+    """Force the first K2 kernel of later batch decodes ('r' ring, 'w' wave;
     '' = automatic).  Tests and A/B measurement only."""
     _check(_lib().ez_select_decompress_kernel(ord(kind) if kind else 0))
 
@@ -547,7 +547,7 @@ def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=Non
                      workspace=None, exact_only: bool = False, stream=None, max_len: int = 0):
     """K2: decode complete streams comp[comp_off[s]:comp_off[s+1]] into
     out[out_off[s]:out_off[s+1]] -> (out, sizes, status).  exact_only skips
-    the lane-per-stream fast decoder (every stream on the exact decoder)."""
+    the fast decoders (every stream on the exact decoder)."""
     import torch
 
     _need_cuda(comp, comp_off, out_off)

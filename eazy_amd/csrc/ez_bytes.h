@@ -43,8 +43,18 @@ EZ_HD V16 shl16(V16 v, uint32_t k) {
     const uint64_t hi = n < 64 ? shl64(v.hi, n) | shr64(v.lo, 64 - n) : shl64(v.lo, n - 64);
     return {n < 64 ? shl64(v.lo, n) : 0, hi};
 }
-// 16 bytes at y, clamped into [lo, hi) (hi - lo >= 16): bytes outside read as 0
+// 16 bytes at y, clamped into [lo, hi): bytes outside read as 0 (a range shorter than 16 bytes
+// is read byte by byte: one 16-byte load would leave it)
 EZ_HD V16 ld_clamped(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
+    if (hi - lo < 16) {
+        V16 v{0, 0};
+        for (int t = 0; t < 16; t++) {
+            const uint64_t b = (y + t >= lo && y + t < hi) ? y[t] : 0;
+            if (t < 8) v.lo |= b << (8 * t);
+            else v.hi |= b << (8 * (t - 8));
+        }
+        return v;
+    }
     const uint8_t *yc = y < lo ? lo : (y > hi - 16 ? hi - 16 : y);
     const V16 v = ld16v(yc);
     const int64_t d = y - yc;

@@ -582,14 +582,14 @@ extern "C" int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_le
 }
 
 extern "C" int ez_select_compress_kernel(int kind) {
-    if (kind != 0 && !strchr("sStrlgfw", kind)) return EZ_EINVAL;
+    if (kind != 0 && !strchr("sSw", kind)) return EZ_EINVAL;
     ez::select_split_table(kind == 'S');
     ez::select_compress_variant(kind == 'S' ? 's' : kind);
     return EZ_OK;
 }
 
 extern "C" int ez_select_decompress_kernel(int kind) {
-    if (kind != 0 && kind != 'f' && kind != 'g' && kind != 'r' && kind != 'w') return EZ_EINVAL;
+    if (kind != 0 && kind != 'r' && kind != 'w') return EZ_EINVAL;
     ez::select_decompress_variant(kind);
     return EZ_OK;
 }

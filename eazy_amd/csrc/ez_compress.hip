@@ -532,14 +532,17 @@ hipError_t launch_variant(const CompressArgs &a, hipStream_t st, size_t lds, uns
 
 uint64_t compress_scratch_words(const CompressArgs &a) {
     const char v = compress_variant(a);
-    if (v == 'l') return (lane_scratch_halves(a) + 1) / 2;
     if (v == 's') return split_scratch_words(a);
-    if (v != 'w' || a.hs <= kHtLdsMax) return 0;
+    if (a.hs <= kHtLdsMax) return 0;
     const uint64_t grid = a.count < 2048 ? a.count : 2048;
     return grid * (uint64_t)a.hs;
 }
 
-// K1 variant choice: EZ_K1=lane|g16|grp|tile|wave|general overrides (A/B measurement)
+// K1 choice.  Fresh streams with 2n <= block and a table of at most 4096 entries take K1s
+// (ez_compress_split.hip: the parse kernel + the token writer); everything else -- writer handles
+// (rings), Writes longer than half the window (C4), large tables -- takes the general
+// wave-per-stream kernel below.  EZ_K1=general or ez_select_compress_kernel('w') forces the
+// general kernel (tests, A/B).
 static int g_forced_variant = -1;  // -1: not read yet; 0: automatic; else the kernel's letter
 void select_compress_variant(int v) { g_forced_variant = v; }
 
@@ -547,36 +550,15 @@ char compress_variant(const CompressArgs &a) {
     int &forced = g_forced_variant;
     if (forced < 0) {
         const char *e = getenv("EZ_K1");
-        const std::string v = e ? e : "";
-        forced = v == "lane" ? 'l' : v == "g16" ? 'g' : v == "grp" ? 'r' : v == "tile" ? 't' : v == "split" ? 's' : v == "wave" ? 'f' : v == "general" ? 'w' : 0;
+        forced = e && std::string(e) == "general" ? 'w' : 0;
     }
-    const bool lane = lane_scratch_halves(a) != 0, g16 = g16_stride_words(a) != 0, fresh = fresh_stride_words(a, 64) != 0;
-    const bool grp = grp_stride_words(a) != 0, tile = tile_stride_words(a) != 0, split = split_stride_words(a) != 0;
-    if (forced == 's' && split) return 's';
-    if (forced == 't' && tile) return 't';
-    if (forced == 'r' && grp) return 'r';
-    if (forced == 'l' && lane) return 'l';
-    if (forced == 'g' && g16) return 'g';
-    if (forced == 'f' && fresh) return 'f';
     if (forced == 'w') return 'w';
-    if (split) return 's';  // fresh streams: parse kernel + token-writer kernel
-    if (tile) return 't';  // fresh streams: G lanes per stream, one exchange per window
-    if (grp) return 'r';  // fresh streams: G lanes per stream, LDS-staged (fastest at C1)
-    if (lane && a.count >= 16384) return 'l';  // enough streams to fill the chip one lane each
-    if (g16) return 'g';
-    if (fresh) return 'f';
-    return 'w';
+    return split_stride_words(a) != 0 ? 's' : 'w';
 }
 
 hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;
-    const char v = compress_variant(a);
-    if (v == 'l') return launch_compress_lane(a, (uint16_t *)a.ht_global, st);
-    if (v == 'g') return launch_compress_g16(a, st);
-    if (v == 't') return launch_compress_tile(a, st);
-    if (v == 's') return launch_compress_split(a, a.ht_global, st);
-    if (v == 'r') return launch_compress_grp(a, st);
-    if (v == 'f') return launch_compress_fresh(a, st, 64);
+    if (compress_variant(a) == 's') return launch_compress_split(a, a.ht_global, st);
     const bool htl = a.hs <= kHtLdsMax;
     const bool pl = a.max_len > 0 && (int64_t)a.max_len <= kPLdsMax;
     const bool ring = a.ring != nullptr;

@@ -8,7 +8,7 @@
 // Why two kernels.  The parse is a serial chain per stream: every window's
 // decision needs the table after the previous one.  Writing the tokens
 // (Encoder.Tag/Offset :537-597, appendLiteral/appendCopy :519-527) does not
-// feed back into that chain, but done inside it (K1t) it puts the literal
+// feed back into that chain, but done inside it (a one-kernel form, round 1) it puts the literal
 // loads, the encodes and the stores on every iteration's critical path.  Here
 //   K1p (G lanes per stream, the table in LDS) runs only the chain: visit,
 //       capped judgement, exact extension of an accepted match, the i+1
@@ -683,7 +683,10 @@ __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride
         int32_t slot = 0;
         if (edge_stream && lj == 0) slot = (int32_t)atomicAdd((uint32_t *)(edge + 128 + kEdgeSlots * edge_slot_bytes(A)), 1u);
         slot = bcast(slot, G * g);
-        if (edge_stream && slot >= kEdgeSlots) err = EZ_ESTUCK;  // cannot happen (20 slots suffice)
+        if (edge_stream && slot >= kEdgeSlots) {  // cannot happen (20 slots suffice)
+            err = EZ_ESTUCK;
+            p = edge + 16;
+        }
         if (edge_stream && !err) {
             uint8_t *d = edge + 128 + (uint64_t)slot * edge_slot_bytes(A);
             for (int32_t k = lj; k < n + 80; k += G) d[k] = (k >= 16 && k < n + 16) ? src[k - 16] : (uint8_t)0;
@@ -851,21 +854,12 @@ uint32_t split_stride(const CompressArgs &a) {
     return (uint32_t)w;
 }
 
-bool split_gin() {
-    static const bool v = !(getenv("EZ_K1S_GIN") && atoi(getenv("EZ_K1S_GIN")) == 0);
-    return v;
-}
-
-int split_g() {
-    static const int g = getenv("EZ_K1S_G") ? atoi(getenv("EZ_K1S_G")) : 16;
-    return g == 8 ? 8 : 16;
-}
 // lanes per stream for T32: 32 when the batch has few streams (long Writes, C2: two
 // waves per SIMD instead of one, 33.3 vs 34.3 ms); EZ_K1S_G32=16|32 overrides
 int split_g32(uint64_t count) {
     static const int g = getenv("EZ_K1S_G32") ? atoi(getenv("EZ_K1S_G32")) : 0;
     if (g == 32 || g == 16) return g;
-    return count <= 8192 ? 32 : split_g();
+    return count <= 8192 ? 32 : 16;
 }
 bool g_split_t32 = false;  // ez_select_compress_kernel('S')
 bool split_t32_forced() {
@@ -940,37 +934,55 @@ __global__ void k_lds_store_order(uint32_t *res) {
     if (l < 8 && t[l] != (uint16_t)(56 + l + 1)) atomicAdd(res, 1u);
 }
 
-}  // namespace
+// The property T32 relies on, checked once per process on the device: same-address LDS
+// exchanges of one wave instruction apply in ascending lane order (lane l reads what lane l-4
+// wrote).  If it ever fails, K1s-T32 is not used.
+__global__ void k_lds_order(uint32_t *res) {
+    __shared__ uint32_t t[4];
+    const uint32_t l = threadIdx.x;
+    if (l < 4) t[l] = 0;
+    __syncthreads();
+    const uint32_t old = atomicExch(&t[l & 3], l + 1);
+    const uint32_t want = l < 4 ? 0 : l - 3;
+    if (old != want) atomicAdd(res, 1u);
+}
 
-bool lds_exchange_in_lane_order();
-
-bool lds_store_in_lane_order() {
-    static int ok = -1;
-    if (ok >= 0) return ok == 1;
-    ok = 0;
+// one 64-lane probe kernel on a private stream; true when it reports no violation
+bool lds_probe(void (*kern)(uint32_t *)) {
     uint32_t *d = nullptr, h = 1;
     hipStream_t st = nullptr;
+    bool ok = false;
     if (hipMalloc(&d, sizeof(uint32_t)) != hipSuccess) return false;
     if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) == hipSuccess) {
         if (hipMemsetAsync(d, 0, sizeof(uint32_t), st) == hipSuccess) {
-            hipLaunchKernelGGL(k_lds_store_order, dim3(1), dim3(64), 0, st, d);
+            hipLaunchKernelGGL(kern, dim3(1), dim3(64), 0, st, d);
             if (hipGetLastError() == hipSuccess && hipMemcpyAsync(&h, d, sizeof(uint32_t), hipMemcpyDeviceToHost, st) == hipSuccess &&
                 hipStreamSynchronize(st) == hipSuccess)
-                ok = h == 0 ? 1 : 0;
+                ok = h == 0;
         }
         (void)hipStreamDestroy(st);
     }
     (void)hipFree(d);
-    return ok == 1;
+    return ok;
+}
+
+}  // namespace
+
+bool lds_exchange_in_lane_order() {
+    static const bool ok = lds_probe(k_lds_order);
+    return ok;
+}
+
+bool lds_store_in_lane_order() {
+    static const bool ok = lds_probe(k_lds_store_order);
+    return ok;
 }
 
 // the table the batch takes: 16 (T16), 32 (T32) or 0 (K1s cannot take it)
 static int split_table(const CompressArgs &a) {
     if (a.count > (1ull << 31)) return 0;
-    const int G = split_g();
-    if (!split_t32_forced() && (G == 8 ? split_stride<8, true, true>(a) : split_stride<16, true, true>(a)) != 0 && lds_store_in_lane_order())
-        return 16;
-    if ((G == 8 ? split_stride<8, false, true>(a) : split_stride<16, false, true>(a)) != 0 && lds_exchange_in_lane_order()) return 32;
+    if (!split_t32_forced() && split_stride<16, true, true>(a) != 0 && lds_store_in_lane_order()) return 16;
+    if (split_stride<16, false, true>(a) != 0 && lds_exchange_in_lane_order()) return 32;
     return 0;
 }
 
@@ -981,21 +993,20 @@ uint32_t split_stride_words(const CompressArgs &a) { return split_table(a) != 0 
 // records (8 bytes per record slot entry), then k1_lean's edge area
 uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a) * 2 + (edge_area_bytes(a) + 3) / 4; }
 
+// K1s routing: one Write per stream on the u16 table -> k1_lean (EZ_K1S_LEAN=0: k1_parse, the
+// previous form, kept for A/B); multi-Write streams and the u32 table (streams over 64 KiB, or
+// forced) -> k1_parse, 32 lanes per stream for batches of few streams
 hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t st) {
     uint64_t *recs = (uint64_t *)scratch;
-    const int G = split_g(), T = split_table(a);
-    if (a.write_idx) {  // multi-Write streams: inputs through L1/L2
-        if (T == 16) return G == 8 ? launch_split_g<8, true, true, true>(a, recs, st) : launch_split_g<16, true, true, true>(a, recs, st);
+    const int T = split_table(a);
+    if (a.write_idx) {
+        if (T == 16) return launch_split_g<16, true, true, true>(a, recs, st);
         if (split_g32(a.count) == 32) return launch_split_g<32, false, true, true>(a, recs, st);
-        return G == 8 ? launch_split_g<8, false, true, true>(a, recs, st) : launch_split_g<16, false, true, true>(a, recs, st);
+        return launch_split_g<16, false, true, true>(a, recs, st);
     }
-    // EZ_K1S_GIN=0 (experiments): inputs staged in LDS when they fit
-    const bool lds_in = !split_gin() && (G == 8 ? split_stride<8, true, false>(a) : split_stride<16, true, false>(a)) != 0;
-    if (T == 16 && lds_in) return G == 8 ? launch_split_g<8, true, false, false>(a, recs, st) : launch_split_g<16, true, false, false>(a, recs, st);
-    if (T == 16 && G == 16 && split_lean()) return launch_lean(a, recs, st);
-    if (T == 16) return G == 8 ? launch_split_g<8, true, true, false>(a, recs, st) : launch_split_g<16, true, true, false>(a, recs, st);
+    if (T == 16) return split_lean() ? launch_lean(a, recs, st) : launch_split_g<16, true, true, false>(a, recs, st);
     if (split_g32(a.count) == 32) return launch_split_g<32, false, true, false>(a, recs, st);
-    return G == 8 ? launch_split_g<8, false, true, false>(a, recs, st) : launch_split_g<16, false, true, false>(a, recs, st);
+    return launch_split_g<16, false, true, false>(a, recs, st);
 }
 
 }  // namespace ez

@@ -179,162 +179,6 @@ __device__ int d_read_loop(Dec &d, int64_t plen, int64_t *i, int64_t *nout, bool
 }
 
 
-// ---------------------------------------------------------------------------
-// K2-fast: one lane per stream (batch mode).  A lane parses its stream's
-// tokens serially and expands them with 16-byte moves; 64 streams advance in
-// parallel per wave, so the per-token parse cost is shared by 64 tokens.
-// It restates the same reader.go semantics for the common case only: header
-// metas (magic / version 0 / reset before any output), padding, breaks
-// (skipped), literal and copy tokens.  Any other condition — an error of any
-// kind, a mid-stream MetaReset, an unsupported or wide meta, a length over
-// BlockSizeLimit, a full output slot, a truncated token — hands the stream to
-// the exact wave-per-stream decoder (k2_decompress over A.slow), which
-// recomputes it from scratch.
-//
-// Lanes of a wave sit at different points of different streams, so the loop
-// body is written to be uniform: every lane runs the same instruction
-// sequence each iteration (parse by selects, one predicated 16-byte load,
-// one 16-byte store); only rare events (metas, slot tails, errors) branch.
-
-#ifndef EZ_EXP
-#define EZ_EXP 0  // timing experiments only (1: no stores, 2: no data loads, 3: neither)
-#endif
-
-// One iteration = (parse the token whose header was loaded by the previous
-// iteration) + (one 16-byte move).  The move's source load and the next
-// header's load are issued together: a lane waits for memory once per
-// iteration, and the hardware's unaligned loads do all byte alignment.
-// Rare cases (metas, long lengths, runs shorter than 16, references before
-// the slot, the batch's last bytes, slot tails) take branches.
-__device__ __forceinline__ void fast_one(const DecompressArgs &A, const uint64_t s) {
-    const uint8_t *b = A.in + A.in_off[s];
-    const int64_t nb64 = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
-    const uint8_t *in_end = A.in + A.in_off[A.count];  // loads never pass the last stream's end
-    uint8_t *out = A.out + A.out_off[s];
-    const int64_t cap64 = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
-    const int64_t limit = A.block_size_limit;
-    // 32-bit positions; clamped loads need >= 16 input bytes in the batch and a 16-byte slot
-    bool slow = in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16;
-    const int32_t nb = slow ? 0 : (int32_t)nb64, cap = (int32_t)cap64;
-    int32_t i = 0, pos = 0, bsl = -1;  // bsl: log2 of the window after MetaReset (-1: none yet)
-    V16 h{0, 0};                       // 16 bytes at b + i (the next header)
-    if (!slow) h = b + 16 <= in_end ? ld16v(b) : ld_clamped(b, A.in, in_end);
-    // the token being written: rem bytes at out + dst from sp (input or output)
-    int32_t rem = 0, dst = 0, step = 16;
-    const uint8_t *sp = b;
-    bool from_in = false, patt = false;
-    V16 pv{0, 0};
-#if EZ_EXP == 1 || EZ_EXP == 3
-    uint64_t sinkv = 0;
-#endif
-    for (;;) {
-        if (rem == 0) {
-            if (i >= nb) break;
-            const uint64_t lo = h.lo;
-            const uint32_t t0 = (uint32_t)lo & 0xff, l7 = t0 & 0x7f;
-            int32_t adv;
-            if (t0 == 0 || t0 == 0x80) {
-                if (t0 == 0) {  // padding (reader.go:221-224), a run of zero bytes at once
-                    adv = lo ? (int32_t)(__builtin_ctzll(lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
-                } else {
-                    // meta (continueMetaTag reader.go:272-325): header metas and breaks only
-                    const uint32_t mb = (uint32_t)(lo >> 8) & 0xff, mt = mb & 0xf8, ml = mb & 7;
-                    const int32_t mln = ml == 7 ? 0 : (1 << ml);
-                    const uint32_t marg = (uint32_t)(lo >> 16) & 0xff;
-                    const bool m_brk = mt == kMetaBreak && mln == 0;
-                    const bool m_rst = mt == kMetaReset && mln == 1 && marg <= 32 && pos == 0 && (limit == 0 || (1ll << marg) <= limit);
-                    const bool m_ver = mt == kMetaVer && mln == 1 && marg == 0;
-                    const bool m_mag = mt == kMetaMagic && mln == 4 && (uint32_t)(lo >> 16) == 0x797a6165u;
-                    if (ml == 6 || i + 2 + mln > nb || !(m_brk || m_rst || m_ver || m_mag)) { slow = true; break; }
-                    if (m_rst) bsl = (int32_t)marg;
-                    adv = 2 + mln;
-                }
-            } else {
-                // Decoder.Tag reader.go:346-392 and Decoder.Offset :394-420, by selects
-                const uint32_t lx = (uint32_t)(lo >> 8);
-                const int64_t L = l7 < 124 ? (int64_t)l7
-                                : (l7 == 124 ? 124 + (int64_t)(lx & 0xff) : (l7 == 125 ? 380 + (int64_t)(lx & 0xffff) : 65916 + (int64_t)lx));
-                const uint32_t j = l7 < 124 ? 1 : (l7 == 124 ? 2 : (l7 == 125 ? 3 : 5));
-                const bool cp = (t0 & 0x80) != 0;
-                const uint64_t x = fun8(lo, h.hi, j);  // bytes from the offset on (header <= 11 bytes)
-                const bool lng = (x & 0xff) == 0xff;
-                const uint64_t y = lng ? fun8(lo, h.hi, j + 1) : x;
-                const uint32_t o = (uint32_t)y & 0xff, ox = (uint32_t)(y >> 8);
-                const int64_t D0 = o < 252 ? (int64_t)o : (o == 252 ? 252 + (int64_t)(ox & 0xff) : (o == 253 ? 508 + (int64_t)(ox & 0xffff) : 66044 + (int64_t)ox));
-                const uint32_t k = o < 252 ? 1 : (o == 252 ? 2 : (o == 253 ? 3 : 5));
-                const int64_t D = lng ? D0 : D0 + L;
-                adv = cp ? (int32_t)(j + (lng ? 1 : 0) + k) : (int32_t)(j + L);
-                const int64_t bs = bsl < 0 ? 0 : (1ll << bsl);
-                const bool bad = l7 == 127 || (cp && o == 255) || (limit != 0 && L > limit) || bs == 0 ||
-                                 pos + L > cap || (int64_t)i + (cp ? (int64_t)adv : (int64_t)j + L) > nb || (cp && D > bs);
-                if (bad) { slow = true; break; }  // the exact decoder takes the stream
-                dst = pos;
-                rem = (int32_t)L;
-                pos += (int32_t)L;
-                from_in = !cp;
-                sp = cp ? out + (dst - (int32_t)D) : b + (i + (int32_t)j);
-                patt = cp && D < 16;
-                step = 16;
-                if (patt) {
-                    // zero region (D == 0, reader.go:176-179) or a short-period run:
-                    // one 16-byte pattern stored every `step` bytes
-                    if (D == 0) {
-                        pv = V16{0, 0};
-                    } else {
-                        const uint32_t per = (uint32_t)D;
-                        pv = run_pattern(shr16(ld_clamped(out + dst - 16, out, out + cap), 16 - per), per);
-                        step = (int32_t)(per * (16 / per));
-                    }
-                }
-            }
-            i += adv;
-            // the next header, loaded beside this token's first move
-            if (i < nb) h = b + i + 16 <= in_end ? ld16v(b + i) : ld_clamped(b + i, A.in, in_end);
-        }
-        if (rem > 0) {
-            V16 v;
-#if EZ_EXP != 2 && EZ_EXP != 3
-            // inputs near the batch end / references before the slot read zeros there (rare)
-            if (from_in ? sp + 16 > in_end : sp < out) v = from_in ? ld_clamped(sp, A.in, in_end) : ld_clamped(sp, out, out + cap);
-            else v = ld16v(sp);
-#else
-            v = V16{(uint64_t)sp, h.lo};
-#endif
-            if (patt) v = pv;
-#if EZ_EXP != 1 && EZ_EXP != 3
-            if (rem >= 16 || dst + 16 <= cap) st16v(out + dst, v);
-            else put_small(out + dst, v, (uint32_t)rem);
-#else
-            sinkv ^= v.lo;
-#endif
-            const int32_t kk = rem < step ? rem : step;
-            dst += kk;
-            sp += kk;
-            rem -= kk;
-        }
-    }
-#if EZ_EXP == 1 || EZ_EXP == 3
-    if (sinkv == 0x123456789ull) pos++;
-#endif
-    if (slow) {
-        const uint32_t at = atomicAdd(&A.slow[0], 1u);
-        A.slow[1 + at] = (uint32_t)s;
-    } else {
-        A.out_size[s] = (uint64_t)pos;
-        if (A.status) A.status[s] = EZ_OK;
-    }
-}
-
-// grid-stride over streams (EZ_K2_WAVES caps the streams in flight, experiments)
-// spw: streams per wave (64 = every lane; fewer = more waves per SIMD to hide latency)
-__global__ __launch_bounds__(256) void k2_fast(DecompressArgs A, uint32_t spw) {
-    const uint64_t todo = A.todo ? (uint64_t)A.todo[0] : A.count;
-    const uint32_t l = threadIdx.x & 63;
-    if (l >= spw) return;
-    const uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t k = w * spw + l; k < todo; k += nw * spw) fast_one(A, A.todo ? (uint64_t)A.todo[1 + k] : k);
-}
-
 __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
     const int lane = lane_id();
     const uint64_t todo = A.slow ? (uint64_t)A.slow[0] : A.count;
@@ -392,8 +236,9 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
 
 }  // namespace
 
-// two stream lists: K2g -> k2_fast hand-overs, k2_fast -> exact decoder hand-overs
-static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'f', 'g', 'r', 'w'
+// the batch decoders: K2r (ring, slots < 64 KiB) or K2w (wave per stream, longer slots), each
+// handing the streams it does not finish to the exact decoder; 'r' / 'w' force one (tests, A/B)
+static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'r', 'w'
 void select_decompress_variant(int v) { g_decompress_variant = v; }
 
 uint64_t decompress_workspace_words(uint64_t count) { return 2 * count + 32; }
@@ -419,7 +264,7 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     if (e != hipSuccess) return e;
     if (g_decompress_variant < 0) {
         const char *v = getenv("EZ_K2");
-        g_decompress_variant = v && strcmp(v, "group") == 0 ? 'g' : (v && strcmp(v, "fast") == 0 ? 'f' : (v && strcmp(v, "wave") == 0 ? 'w' : 0));
+        g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w' : (v && strcmp(v, "ring") == 0 ? 'r' : 0);
     }
     if (g_decompress_variant == 'w' || (g_decompress_variant == 0 && a.max_out >= long_slot)) {
         // long streams (slots of 64 KiB and more, C2/C4): too few to give every lane one;
@@ -430,44 +275,10 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
         return hipGetLastError();
     }
-    // K2g (LDS group decoder) first when the slots are small; its hand-overs go
-    // through k2_fast, whose hand-overs go to the exact decoder
-    // K2g is opt-in: at C1 the lane-per-stream decoder is faster
-    const uint32_t RG = g_decompress_variant == 'g' ? group_decode_region(a.max_out) : 0;
-    if (RG) {
-        uint32_t *list2 = a.slow + a.count + 16;
-        e = hipMemsetAsync(list2, 0, sizeof(uint32_t), st);
-        if (e != hipSuccess) return e;
-        e = launch_decompress_group(a, RG, st);
-        if (e != hipSuccess) return e;
-        DecompressArgs f = a;
-        f.todo = a.slow;
-        f.slow = list2;
-        const uint64_t fgrid = (a.count + 255) / 256;
-        hipLaunchKernelGGL(k2_fast, dim3((unsigned)fgrid), dim3(256), 0, st, f, 64u);
-        e = hipGetLastError();
-        if (e != hipSuccess) return e;
-        const uint64_t grid = a.count < 4096 ? a.count : 4096;
-        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, f);
-        return hipGetLastError();
-    }
-    if (g_decompress_variant != 'f') {
-        // K2r (default): k2_fast with the recent output in an LDS ring
-        e = launch_decompress_ring(a, st);
-        if (e != hipSuccess) return e;
-        const uint64_t grid = a.count < 4096 ? a.count : 4096;
-        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
-        return hipGetLastError();
-    }
-    static const unsigned blk = getenv("EZ_K2_BLOCK") ? (unsigned)atoi(getenv("EZ_K2_BLOCK")) : 256u;
-    static const uint64_t maxw = getenv("EZ_K2_WAVES") ? (uint64_t)atoll(getenv("EZ_K2_WAVES")) : 0;
-    static const uint32_t spw = getenv("EZ_K2_SPW") ? (uint32_t)atoi(getenv("EZ_K2_SPW")) : 64u;
-    const uint64_t lanes = (a.count + spw - 1) / spw * 64;  // threads launched
-    uint64_t fgrid = (lanes + blk - 1) / blk;
-    if (maxw && fgrid * blk / 64 > maxw) fgrid = (maxw * 64 + blk - 1) / blk;
-    hipLaunchKernelGGL(k2_fast, dim3((unsigned)fgrid), dim3(blk), 0, st, a, spw);
-    // exact decoder over the handed-over streams (count read on the device)
-    uint64_t grid = a.count < 4096 ? a.count : 4096;
+    // K2r (default): one lane per stream with the recent output in an LDS ring
+    e = launch_decompress_ring(a, st);
+    if (e != hipSuccess) return e;
+    const uint64_t grid = a.count < 4096 ? a.count : 4096;
     hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
     return hipGetLastError();
 }

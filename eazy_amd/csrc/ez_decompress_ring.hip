@@ -3,11 +3,11 @@
 //
 // Restates Reader.Read to EOF for NewReaderBytes (reader.go:116-216 read,
 // readTag :218-270, continueMetaTag :272-325, reset :327-344, Decoder
-// :346-514) for the common case, exactly as k2_fast (ez_decompress.hip) does —
-// header metas, padding, breaks, literal and copy tokens; anything else hands
-// the stream to the exact decoder — and differs in where a copy reads from.
+// :346-514) for the common case — header metas, padding, breaks, literal and
+// copy tokens; anything else hands the stream to the exact decoder.
 //
-// Why.  k2_fast reads every back-reference from the output it wrote to HBM a
+// Why the ring.  A lane decoder without it (k2_fast, round 1; removed) read every
+// back-reference from the output it wrote to HBM a
 // few tokens earlier; 64 lanes of a wave touch 64 unrelated streams, and at
 // C1 the 8,192 streams in flight per XCD keep ~5 MB of recently written lines
 // live against a 4 MB L2 (PMC: 43 % L2 misses).  Most distances are short

@@ -67,47 +67,30 @@ struct DecompressArgs {
     DecodeState *st;          // handle: state in/out
     uint32_t *slow;           // batch: [0] = count, [1..] = streams the fast path handed over (nullptr = exact path only)
     uint64_t max_out;         // batch: host hint, largest output slot (0 = unknown)
-    const uint32_t *todo;     // batch, k2_fast: [0] = count, [1..] = the streams to decode (nullptr = all)
+    const uint32_t *todo;     // batch: [0] = count, [1..] = the streams to decode (nullptr = all)
 };
 
 // words of workspace the two-level batch decoder needs
 uint64_t decompress_workspace_words(uint64_t count);
 
 hipError_t launch_compress(const CompressArgs &a, hipStream_t s);
-// K1f: fresh streams with n <= block (ez_compress_fresh.hip); G = lanes per stream
-uint32_t fresh_stride_words(const CompressArgs &a, int G);
-hipError_t launch_compress_fresh(const CompressArgs &a, hipStream_t s, int G);
-// K1l: fresh streams, one lane per stream (ez_compress_lane.hip); u16 scratch count*hs
-uint32_t grp_stride_words(const CompressArgs &a);
-hipError_t launch_compress_grp(const CompressArgs &a, hipStream_t s);
-uint64_t lane_scratch_halves(const CompressArgs &a);
-hipError_t launch_compress_lane(const CompressArgs &a, uint16_t *scratch, hipStream_t s);
-// K1t: fresh streams, G lanes per stream, exchange-based visits (ez_compress_tile.hip)
-uint32_t tile_stride_words(const CompressArgs &a);
-bool lds_exchange_in_lane_order();  // the hardware property K1t relies on (checked once)
-hipError_t launch_compress_tile(const CompressArgs &a, hipStream_t s);
 // K1s: fresh streams, parse kernel + token-writer kernel (ez_compress_split.hip);
 // scratch = 16-byte match records, split_scratch_words u32 words
 uint32_t split_stride_words(const CompressArgs &a);
 uint64_t split_scratch_words(const CompressArgs &a);
 void select_split_table(bool t32);  // force the u32 exchange table (tests, A/B)
 hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t s);
-// the K1 variant a batch launch takes: 'l' lane, 'g' g16, 'f' fresh wave, 'w' general wave
+// the K1 kernel a batch launch takes: 's' K1s (parse + token writer), 'w' general wave per stream
 char compress_variant(const CompressArgs &a);
 void select_compress_variant(int v);  // 0 = automatic, else a variant letter (tests, A/B)
-// K1g: fresh streams, 16 lanes per stream (ez_compress_g16.hip)
-uint32_t g16_stride_words(const CompressArgs &a);
-hipError_t launch_compress_g16(const CompressArgs &a, hipStream_t s);
 // u32 words of global hash-table scratch a batch launch needs (hs too big for LDS)
 uint64_t compress_scratch_words(const CompressArgs &a);
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t s);
-// K2g: G lanes per stream, compressed bytes and history in LDS (ez_decompress_group.hip)
-uint32_t group_decode_region(uint64_t max_out);
-hipError_t launch_decompress_group(const DecompressArgs &a, uint32_t R, hipStream_t s);
 void select_decompress_variant(int v);
 // K2r: one lane per stream with a 512-byte LDS ring of recent output (ez_decompress_ring.hip)
 hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t s);
-hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t s);  // K2w, long streams  // 0 = automatic, 'f' fast, 'g' group (tests, A/B)
+hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t s);  // K2w, long streams
+bool lds_exchange_in_lane_order();  // the LDS property K1s-T32 relies on (checked once)
 hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
                        uint8_t *packed, uint64_t *packed_off, void *workspace, hipStream_t s);
 size_t pack_workspace(uint64_t count);

@@ -1,7 +1,7 @@
-// ez_k1_common.h — pieces shared by the group-per-stream K1 kernels
-// (ez_compress_grp.hip, ez_compress_tile.hip): a byte view of the stream
-// staged in LDS, group ballots/broadcasts, the branch-free Encoder.Tag /
-// Encoder.Offset (writer.go:537-597) and the cooperative exact match count.
+// ez_k1_common.h — pieces of the group-per-stream K1 kernels (ez_compress_split.hip):
+// byte views of a stream (staged in LDS, or read through L1/L2), group
+// ballots/broadcasts, the branch-free Encoder.Tag / Encoder.Offset
+// (writer.go:537-597) and the cooperative exact match count.
 #pragma once
 
 #include "ez_format.h"

@@ -169,18 +169,17 @@ int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *works
 
 /* Introspection (no reference counterpart): the K1 kernel a batch of `count`
  * fresh streams of <= max_len bytes would run on the current device, as a
- * character: 's' split (parse + token writer), 't' tile (exchange visits), 'r' grp, 'l' lane, 'g' g16,
- * 'f' fresh wave, 'w' general wave; EZ_EDEVICE (negated) without a device. */
+ * character: 's' K1s (parse + token writer; fresh streams with 2n <= block and
+ * at most 4096 table entries), 'w' general wave per stream (everything else);
+ * EZ_EDEVICE (negated) without a device. */
 int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t count);
 /* Testing / A-B measurement (no reference counterpart): force the K1 kernel of
- * later batch calls in this process ('s' split, 'S' split with the u32
- * exchange table, 't' tile, 'r', 'l', 'g', 'f',
- * 'w'; 0 = automatic choice).  A forced kernel that cannot take a batch falls
+ * later batch calls in this process ('s' K1s, 'S' K1s with the u32
+ * exchange table, 'w' general; 0 = automatic choice).  A forced kernel that cannot take a batch falls
  * back to the automatic choice.  Not thread-safe against concurrent calls. */
 int ez_select_compress_kernel(int kind);
 /* Testing / A-B measurement: the first K2 kernel of later batch decodes with a
- * workspace ('r' lane-per-stream with an LDS ring of recent output, 'f'
- * lane-per-stream, 'g' LDS group decoder (needs a max_len hint), 'w' wave per
+ * workspace ('r' lane-per-stream with an LDS ring of recent output, 'w' wave per
  * stream with LDS input and output rings; 0 = automatic: 'w' for slots of 64 KiB
  * and more, else 'r').  Streams either cannot take go on to the exact decoder. */
 int ez_select_decompress_kernel(int kind);

@@ -119,17 +119,22 @@ def test_batch_decoder_errors_match_oracle(cuda):
     torch.cuda.synchronize()
     for out, sizes, status in res:
         _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
-    # the LDS group decoder (K2grp, taken when the largest slot is small) on the same corpus
+    # the ring decoder with a small-slot hint on the same corpus
     cap = 8192
     ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-    out, sizes, status = ez.decompress_batch(comp, coff, ooff, max_len=cap)
-    torch.cuda.synchronize()
-    _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
+    for kind in ("r", "w"):
+        ez.select_decompress_kernel(kind)
+        try:
+            out, sizes, status = ez.decompress_batch(comp, coff, ooff, max_len=cap)
+            torch.cuda.synchronize()
+        finally:
+            ez.select_decompress_kernel("")
+        _cmp_oracle(ins, cap, out.cpu().numpy(), sizes.cpu().numpy(), status.cpu().numpy())
 
 
 def test_batch_decoders_on_damaged_streams(cuda):
     """Valid streams truncated, bit-flipped, padded, with breaks and with a
-    second header (MetaReset mid-stream): the group, lane and exact decoders
+    second header (MetaReset mid-stream): the ring, wave and exact decoders
     all give the oracle's bytes and first error."""
     import torch
 
@@ -166,7 +171,7 @@ def test_batch_decoders_on_damaged_streams(cuda):
     coff = torch.from_numpy(offs).to(cuda)
     for cap in (4096, 8192):
         ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-        for kind, kw in (("", {"max_len": cap}), ("f", {"max_len": cap}), ("g", {"max_len": cap}), ("w", {"max_len": cap}), ("", {}),
+        for kind, kw in (("", {"max_len": cap}), ("r", {"max_len": cap}), ("w", {"max_len": cap}), ("", {}),
                          ("", {"exact_only": True})):
             ez.select_decompress_kernel(kind)
             try:
