@@ -268,6 +268,13 @@ extern "C" int ez_writer_set_version(ez_writer *w, int ver) {
 
 extern "C" int ez_writer_is_reset(const ez_writer *w) { return w->pristine ? 1 : 0; }
 
+// testing hook: w.pos of a handle, ring and table unchanged (positions past 2^32)
+extern "C" int ez_writer_set_position(ez_writer *w, int64_t pos) {
+    if (pos < 0) return EZ_EINVAL;
+    w->pos = pos;
+    return EZ_OK;
+}
+
 extern "C" int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t *out, size_t cap, size_t *out_n) {
     *out_n = 0;
     const size_t bound = ez_compress_bound(n);
@@ -533,9 +540,11 @@ static int compress_batch_impl(int64_t block, int64_t htable, int flags, const e
     a.write_idx = write_idx;
     a.write_end = write_end;
     a.max_writes = max_writes;
-    // multi-Write streams run on K1s only (fresh streams, 2 x stream <= block)
-    if (write_idx && (b->count == 0 || ez::split_stride_words(a) == 0)) return b->count == 0 ? EZ_OK : EZ_EINVAL;
-    const uint64_t words = write_idx ? ez::split_scratch_words(a) : ez::compress_scratch_words(a);
+    // multi-Write streams: K1s when it takes them (fresh streams, 2 x stream <= block), else the
+    // general kernel (one wave per stream, the history read from the stream's earlier Writes)
+    if (write_idx && b->count == 0) return EZ_OK;
+    const bool split_mw = write_idx && ez::split_stride_words(a) != 0;
+    const uint64_t words = split_mw ? ez::split_scratch_words(a) : ez::compress_scratch_words(a);
     if (words) {
         int dev = 0;
         EZ_HIP(hipGetDevice(&dev));
@@ -544,7 +553,7 @@ static int compress_batch_impl(int64_t block, int64_t htable, int flags, const e
         if (sc.ht.ensure((size_t)words * 4)) return EZ_EDEVICE;
         a.ht_global = sc.ht.as<uint32_t>();
     }
-    if (write_idx) EZ_HIP(ez::launch_compress_split(a, a.ht_global, (hipStream_t)hip_stream));
+    if (split_mw) EZ_HIP(ez::launch_compress_split(a, a.ht_global, (hipStream_t)hip_stream));
     else EZ_HIP(ez::launch_compress(a, (hipStream_t)hip_stream));
     return EZ_OK;
 }

@@ -130,11 +130,21 @@ template <bool PL, bool HTL, bool RING>
 __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem) {
     const int lane = lane_id();
     const uint64_t ib = A.in_off[s];
-    const int64_t n = (int64_t)(A.in_off[s + 1] - ib);
+    // multi-Write streams (A.write_idx, fresh streams only): Writes k = write_idx[s] ..
+    // write_idx[s+1]-1 of one Writer, Write k ending at in[write_end[k]]; each Write's loop runs to
+    // its own end (writer.go:213) and the table and the history carry over (writer.go:40-45)
+    const bool mw = !RING && A.write_idx != nullptr;
+    uint64_t wk = 0, wlast = 0;
+    if (mw) {
+        wk = A.write_idx[s];
+        wlast = A.write_idx[s + 1];
+    }
+    uint64_t wbeg = ib;  // the current Write's first byte (index into A.in)
+    int64_t n = (int64_t)((mw ? (wk < wlast ? A.write_end[wk] : ib) : A.in_off[s + 1]) - ib);
     const int64_t bs = A.bs, mask = bs - 1;
     const int64_t hs = A.hs;
     const unsigned hsh = 32u - (unsigned)(64 - __builtin_clzll((uint64_t)(hs - 1)));
-    const int64_t start = A.start;
+    int64_t start = A.start;  // stream position of the current Write's first byte
     const uint8_t *ring = A.ring;
 
     // ---- LDS carve (all offsets 16-aligned)
@@ -191,10 +201,11 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         put_hdr(o, h, lane);
     }
 
-    // block[y & mask] as seen while w.pos == wpos
+    // block[y & mask] as seen while w.pos == wpos; a multi-Write stream's earlier
+    // Writes are the bytes before P.g in the same batch
     auto ringb = [&](int64_t y, int64_t wpos) -> uint32_t {
         const int64_t q = wpos - bs + ((y - wpos) & mask);
-        if (q >= start) return P.b(q - start);
+        if (q >= start || (mw && q >= 0)) return P.b(q - start);
         if (RING) return ring[q & mask];
         return 0u;
     };
@@ -212,289 +223,301 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         const int64_t r = (y - wpos) & mask;
         if (r + 7 >= bs) return false;  // wraps inside the 8 bytes
         const int64_t q = wpos - bs + r;
-        if (q >= start) { v = s8(q - start); return true; }
-        if (!RING && q + 8 <= start) { v = 0; return true; }
+        if (q >= start || (mw && q >= 0)) { v = s8(q - start); return true; }
+        if (!RING && q + 8 <= (mw ? 0 : start)) { v = 0; return true; }
         return false;
     };
 
-    int64_t done = 0, i = 0;
-    int64_t guard = 0;
-    const int64_t guard_max = 16 * n + 4096;
-    // global input: the 16 bytes x-8 .. x+7 around each lane's position, and those of
-    // the window after this one if nothing is accepted (loaded while this one is judged)
-    const bool pf = !PL && in_hi - in_lo >= 16;
-    auto around = [&](int64_t y) -> V16 {
-        const uint8_t *q = P.g + y - 8;
-        return q >= in_lo && q + 16 <= in_hi ? ld16v(q) : ld_clamped(q, in_lo, in_hi);
-    };
-    V16 nxt_w{0, 0};
-    int64_t nxt_i = -1;
-    const bool usefp = FP && pf && start == 0;
-    if (usefp) {  // the zero entries hold stream position 0
-        const V16 z = around(0);
-        for (int64_t k = lane; k < hs; k += kWave) fp[k] = z;
-        __syncthreads();
-    }
-
-    while (i + 4 <= n && !o.err) {
-        if (++guard > guard_max) { o.err = EZ_ESTUCK; break; }
-        const int64_t wpos = start + done;
-        const int64_t rem = n - 3 - i;
-        const int nvalid = rem < kWave ? (int)rem : kWave;
-        const int64_t x = i + lane;
-        const bool valid = lane < nvalid;
-        V16 cur{0, 0};  // bytes x-8 .. x+7 (pf)
-        if (pf) {
-            cur = nxt_i == i ? nxt_w : around(x);
-            nxt_w = around(x + nvalid);
-            nxt_i = i + nvalid;
+    for (;;) {  // the stream's Writes (one unless mw)
+        int64_t done = 0, i = 0;
+        int64_t guard = 0;
+        const int64_t guard_max = 16 * n + 4096;
+        // global input: the 16 bytes x-8 .. x+7 around each lane's position, and those of
+        // the window after this one if nothing is accepted (loaded while this one is judged)
+        const bool pf = !PL && in_hi - in_lo >= 16;
+        auto around = [&](int64_t y) -> V16 {
+            const uint8_t *q = P.g + y - 8;
+            return q >= in_lo && q + 16 <= in_hi ? ld16v(q) : ld_clamped(q, in_lo, in_hi);
+        };
+        V16 nxt_w{0, 0};
+        int64_t nxt_i = -1;
+        const bool usefp = FP && pf && start == 0;
+        if (usefp) {  // the zero entries hold stream position 0
+            const V16 z = around(0);
+            for (int64_t k = lane; k < hs; k += kWave) fp[k] = z;
+            __syncthreads();
         }
 
-        // -- hash + intra-window predecessor / successor with the same hash
-        uint32_t h = 0xffffffffu;
-        if (valid) h = ((pf ? (uint32_t)cur.hi : P.u32(x)) * kHashMul) >> hsh;
-        const int bk = (int)(h & (kBuckets - 1));
-        if (valid) {
-            atomicOr((unsigned long long *)&bmask[bk], 1ull << lane);
-            H[lane] = h;
-        }
-        __syncthreads();
-        int prev = -1, next = kWave;
-        if (valid) {
-            const uint64_t m = bmask[bk];
-            uint64_t below = m & ((1ull << lane) - 1);
-            while (below) {
-                const int k = 63 - __builtin_clzll(below);
-                if (H[k] == h) { prev = k; break; }
-                below &= ~(1ull << k);
+        while (i + 4 <= n && !o.err) {
+            if (++guard > guard_max) { o.err = EZ_ESTUCK; break; }
+            const int64_t wpos = start + done;
+            const int64_t rem = n - 3 - i;
+            const int nvalid = rem < kWave ? (int)rem : kWave;
+            const int64_t x = i + lane;
+            const bool valid = lane < nvalid;
+            V16 cur{0, 0};  // bytes x-8 .. x+7 (pf)
+            if (pf) {
+                cur = nxt_i == i ? nxt_w : around(x);
+                nxt_w = around(x + nvalid);
+                nxt_i = i + nvalid;
             }
-            uint64_t above = lane == 63 ? 0ull : (m & (~0ull << (lane + 1)));
-            while (above) {
-                const int k = __builtin_ctzll(above);
-                if (H[k] == h) { next = k; break; }
-                above &= above - 1;
-            }
-        }
-        int64_t cand = 0;
-        if (valid) cand = prev >= 0 ? (int64_t)(uint32_t)(start + i + prev) : (int64_t)ht[h];
-        // the candidate's bytes cand-8 .. cand+7 (usefp): an earlier lane's, or the table's
-        V16 cv{0, 0};
-        if (usefp) {
-            const int src = prev >= 0 ? prev : lane;
-            const V16 pv{(uint64_t)__shfl((long long)cur.lo, src, 64), (uint64_t)__shfl((long long)cur.hi, src, 64)};
-            if (valid) cv = prev >= 0 ? pv : fp[h];
-        }
 
-        // -- per-lane capped evaluation
-        int kind = kReject;
-        bool exact = true;
-        int64_t v_st = 0, v_ist = 0, v_iend = 0;
-        if (valid) {
-            const int64_t off = cand - wpos;
-            if (-off > bs) {
-                kind = kReject;  // far skip (writer.go:221-224)
-            } else if (off >= 0 && x > done + off) {
-                // runlen (writer.go:227-231 -> writeRunlen :441-489)
-                const int64_t st = done + off;
-                v_st = st;
-                if (st + 8 < n && (usefp ? cv.hi == 0 : (P.u32(st) == 0 && P.u32(st + 4) == 0))) {
-                    kind = kZero;
+            // -- hash + intra-window predecessor / successor with the same hash
+            uint32_t h = 0xffffffffu;
+            if (valid) h = ((pf ? (uint32_t)cur.hi : P.u32(x)) * kHashMul) >> hsh;
+            const int bk = (int)(h & (kBuckets - 1));
+            if (valid) {
+                atomicOr((unsigned long long *)&bmask[bk], 1ull << lane);
+                H[lane] = h;
+            }
+            __syncthreads();
+            int prev = -1, next = kWave;
+            if (valid) {
+                const uint64_t m = bmask[bk];
+                uint64_t below = m & ((1ull << lane) - 1);
+                while (below) {
+                    const int k = 63 - __builtin_clzll(below);
+                    if (H[k] == h) { prev = k; break; }
+                    below &= ~(1ull << k);
+                }
+                uint64_t above = lane == 63 ? 0ull : (m & (~0ull << (lane + 1)));
+                while (above) {
+                    const int k = __builtin_ctzll(above);
+                    if (H[k] == h) { next = k; break; }
+                    above &= above - 1;
+                }
+            }
+            int64_t cand = 0;
+            if (valid) cand = prev >= 0 ? (int64_t)(uint32_t)(start + i + prev) : (int64_t)ht[h];
+            // the candidate's bytes cand-8 .. cand+7 (usefp): an earlier lane's, or the table's
+            V16 cv{0, 0};
+            if (usefp) {
+                const int src = prev >= 0 ? prev : lane;
+                const V16 pv{(uint64_t)__shfl((long long)cur.lo, src, 64), (uint64_t)__shfl((long long)cur.hi, src, 64)};
+                if (valid) cv = prev >= 0 ? pv : fp[h];
+            }
+
+            // -- per-lane capped evaluation
+            int kind = kReject;
+            bool exact = true;
+            int64_t v_st = 0, v_ist = 0, v_iend = 0;
+            if (valid) {
+                const int64_t off = cand - wpos;
+                if (-off > bs) {
+                    kind = kReject;  // far skip (writer.go:221-224)
+                } else if (off >= 0 && x > done + off) {
+                    // runlen (writer.go:227-231 -> writeRunlen :441-489)
+                    const int64_t st = done + off;
+                    v_st = st;
+                    if (st + 8 < n && (usefp ? cv.hi == 0 : (P.u32(st) == 0 && P.u32(st + 4) == 0))) {
+                        kind = kZero;
+                    } else {
+                        int f = 0, c = 0;
+                        if (!PL && kCap == 8) {  // 8-byte compares (writeRunlen :449-462, capped)
+                            const uint64_t df = (usefp ? cv.hi : s8(st)) ^ (pf ? cur.hi : s8(x));
+                            const uint64_t db = (usefp ? cv.lo : s8(st - 8)) ^ (pf ? cur.lo : s8(x - 8));
+                            f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
+                            if (f > n - x) f = (int)(n - x);
+                            c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
+                            const int64_t cl = st < x - done ? st : x - done;
+                            if (c > cl) c = (int)cl;
+                        } else {
+                            while (f < kCap && x + f < n && P.b(st + f) == P.b(x + f)) f++;
+                            while (c < kCap && st - 1 - c >= 0 && x - 1 - c >= done && P.b(st - 1 - c) == P.b(x - 1 - c)) c++;
+                        }
+                        const bool capped = f == kCap || c == kCap;
+                        if (!capped && f + c < kMinCopyChunk) kind = kReject;
+                        else if (x - st >= bs - 8) kind = kCut;
+                        else { kind = kRun; exact = !capped; v_ist = x - c; v_iend = x + f; }
+                    }
                 } else {
-                    int f = 0, c = 0;
-                    if (!PL && kCap == 8) {  // 8-byte compares (writeRunlen :449-462, capped)
-                        const uint64_t df = (usefp ? cv.hi : s8(st)) ^ (pf ? cur.hi : s8(x));
-                        const uint64_t db = (usefp ? cv.lo : s8(st - 8)) ^ (pf ? cur.lo : s8(x - 8));
+                    // window match (writer.go:233-301)
+                    int64_t ist = x - 1, st = cand - 1;
+                    int c = 0;
+                    uint64_t rb = 0, rf = 0;
+                    bool vec;
+                    if (usefp && cand - 8 >= start && cand + 8 <= wpos && cand - 8 >= wpos - bs) {
+                        rb = cv.lo;  // block[y & mask] is stream byte y for wpos - bs <= y < wpos
+                        rf = cv.hi;
+                        vec = true;
+                    } else {
+                        vec = !PL && kCap == 8 && ring8(cand - 8, wpos, rb) && ring8(cand, wpos, rf);
+                    }
+                    if (vec) {  // 8-byte compares against the ring image (writer.go:236-259, capped)
+                        const uint64_t db = (pf ? cur.lo : s8(x - 8)) ^ rb;
+                        c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
+                        if (c > x - done) c = (int)(x - done);
+                        ist -= c;
+                        st -= c;
+                    } else {
+                        while (c < kCap && ist >= done && P.b(ist) == ringb(st, wpos)) { ist--; st--; c++; }
+                    }
+                    ist++; st++;
+                    int64_t iend = x, end = cand;
+                    int f = 0;
+                    if (vec) {
+                        const uint64_t df = (pf ? cur.hi : s8(x)) ^ rf;
                         f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
                         if (f > n - x) f = (int)(n - x);
-                        c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
-                        const int64_t cl = st < x - done ? st : x - done;
-                        if (c > cl) c = (int)cl;
+                        iend += f;
+                        end += f;
                     } else {
-                        while (f < kCap && x + f < n && P.b(st + f) == P.b(x + f)) f++;
-                        while (c < kCap && st - 1 - c >= 0 && x - 1 - c >= done && P.b(st - 1 - c) == P.b(x - 1 - c)) c++;
+                        while (f < kCap && iend < n && P.b(iend) == ringb(end, wpos)) { iend++; end++; f++; }
                     }
-                    const bool capped = f == kCap || c == kCap;
-                    if (!capped && f + c < kMinCopyChunk) kind = kReject;
-                    else if (x - st >= bs - 8) kind = kCut;
-                    else { kind = kRun; exact = !capped; v_ist = x - c; v_iend = x + f; }
-                }
-            } else {
-                // window match (writer.go:233-301)
-                int64_t ist = x - 1, st = cand - 1;
-                int c = 0;
-                uint64_t rb = 0, rf = 0;
-                bool vec;
-                if (usefp && cand - 8 >= start && cand + 8 <= wpos && cand - 8 >= wpos - bs) {
-                    rb = cv.lo;  // block[y & mask] is stream byte y for wpos - bs <= y < wpos
-                    rf = cv.hi;
-                    vec = true;
-                } else {
-                    vec = !PL && kCap == 8 && ring8(cand - 8, wpos, rb) && ring8(cand, wpos, rf);
-                }
-                if (vec) {  // 8-byte compares against the ring image (writer.go:236-259, capped)
-                    const uint64_t db = (pf ? cur.lo : s8(x - 8)) ^ rb;
-                    c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
-                    if (c > x - done) c = (int)(x - done);
-                    ist -= c;
-                    st -= c;
-                } else {
-                    while (c < kCap && ist >= done && P.b(ist) == ringb(st, wpos)) { ist--; st--; c++; }
-                }
-                ist++; st++;
-                int64_t iend = x, end = cand;
-                int f = 0;
-                if (vec) {
-                    const uint64_t df = (pf ? cur.hi : s8(x)) ^ rf;
-                    f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
-                    if (f > n - x) f = (int)(n - x);
-                    iend += f;
-                    end += f;
-                } else {
-                    while (f < kCap && iend < n && P.b(iend) == ringb(end, wpos)) { iend++; end++; f++; }
-                }
-                const bool capped = c == kCap || f == kCap;
-                const int64_t blit = wpos - bs;
-                const int64_t bend = blit + (iend - done);
-                int64_t d = bend - st;
-                if (d > 0) { end -= d; iend -= d; }
-                d = (end - bs) - blit;
-                if (d > 0) { end -= d; iend -= d; }
-                if (end - st >= kMinCopyChunk) { kind = kWin; exact = !capped; v_ist = ist; v_iend = iend; }
-                else if (capped) { kind = kWin; exact = false; }
-                else kind = kReject;
-            }
-        }
-
-        // -- first lane that accepts (exact resolution, wave-wide)
-        uint64_t cm = wballot(valid && kind != kReject);
-        const uint64_t exm = wballot(exact);
-        int a = -1, ka = kReject;
-        int64_t xa = 0, sta = 0, ista = 0, ienda = 0, canda = 0;
-        while (cm) {
-            const int l = ffs64(cm);
-            const int kl = rl32(kind, l);
-            const bool ex = (exm >> l) & 1;
-            const int64_t xl = i + l;
-            if (kl == kWin) {
-                const int64_t cl = rl64(cand, l);
-                int64_t ist, iend;
-                if (ex) {
-                    ist = rl64(v_ist, l);
-                    iend = rl64(v_iend, l);
-                } else {
-                    const int64_t bw = coop_count(0, lane, [&](int64_t m) {
-                        return xl - 1 - m >= done && P.b(xl - 1 - m) == ringb(cl - 1 - m, wpos);
-                    });
-                    const int64_t fw = coop_count(0, lane, [&](int64_t m) {
-                        return xl + m < n && P.b(xl + m) == ringb(cl + m, wpos);
-                    });
-                    ist = xl - bw;
-                    int64_t st = cl - bw;
-                    iend = xl + fw;
-                    int64_t end = cl + fw;
+                    const bool capped = c == kCap || f == kCap;
                     const int64_t blit = wpos - bs;
                     const int64_t bend = blit + (iend - done);
                     int64_t d = bend - st;
                     if (d > 0) { end -= d; iend -= d; }
                     d = (end - bs) - blit;
                     if (d > 0) { end -= d; iend -= d; }
-                    if (end - st < kMinCopyChunk) { cm &= cm - 1; continue; }  // maybe -> reject
+                    if (end - st >= kMinCopyChunk) { kind = kWin; exact = !capped; v_ist = ist; v_iend = iend; }
+                    else if (capped) { kind = kWin; exact = false; }
+                    else kind = kReject;
                 }
-                a = l; ka = kWin; xa = xl; canda = cl; ista = ist; ienda = iend;
+            }
+
+            // -- first lane that accepts (exact resolution, wave-wide)
+            uint64_t cm = wballot(valid && kind != kReject);
+            const uint64_t exm = wballot(exact);
+            int a = -1, ka = kReject;
+            int64_t xa = 0, sta = 0, ista = 0, ienda = 0, canda = 0;
+            while (cm) {
+                const int l = ffs64(cm);
+                const int kl = rl32(kind, l);
+                const bool ex = (exm >> l) & 1;
+                const int64_t xl = i + l;
+                if (kl == kWin) {
+                    const int64_t cl = rl64(cand, l);
+                    int64_t ist, iend;
+                    if (ex) {
+                        ist = rl64(v_ist, l);
+                        iend = rl64(v_iend, l);
+                    } else {
+                        const int64_t bw = coop_count(0, lane, [&](int64_t m) {
+                            return xl - 1 - m >= done && P.b(xl - 1 - m) == ringb(cl - 1 - m, wpos);
+                        });
+                        const int64_t fw = coop_count(0, lane, [&](int64_t m) {
+                            return xl + m < n && P.b(xl + m) == ringb(cl + m, wpos);
+                        });
+                        ist = xl - bw;
+                        int64_t st = cl - bw;
+                        iend = xl + fw;
+                        int64_t end = cl + fw;
+                        const int64_t blit = wpos - bs;
+                        const int64_t bend = blit + (iend - done);
+                        int64_t d = bend - st;
+                        if (d > 0) { end -= d; iend -= d; }
+                        d = (end - bs) - blit;
+                        if (d > 0) { end -= d; iend -= d; }
+                        if (end - st < kMinCopyChunk) { cm &= cm - 1; continue; }  // maybe -> reject
+                    }
+                    a = l; ka = kWin; xa = xl; canda = cl; ista = ist; ienda = iend;
+                    break;
+                }
+                a = l; ka = kl; xa = xl; sta = rl64(v_st, l);
+                if (kl == kRun) {
+                    if (ex) {
+                        ista = rl64(v_ist, l);
+                        ienda = rl64(v_iend, l);
+                    } else {
+                        const int64_t jf = coop_count(0, lane, [&](int64_t m) {
+                            return xl + m < n && P.b(sta + m) == P.b(xl + m);
+                        });
+                        const int64_t jb = coop_count(0, lane, [&](int64_t m) {
+                            return sta - 1 - m >= 0 && xl - 1 - m >= done && P.b(sta - 1 - m) == P.b(xl - 1 - m);
+                        });
+                        ista = xl - jb;
+                        ienda = xl + jf;
+                    }
+                }
                 break;
             }
-            a = l; ka = kl; xa = xl; sta = rl64(v_st, l);
-            if (kl == kRun) {
-                if (ex) {
-                    ista = rl64(v_ist, l);
-                    ienda = rl64(v_iend, l);
-                } else {
-                    const int64_t jf = coop_count(0, lane, [&](int64_t m) {
-                        return xl + m < n && P.b(sta + m) == P.b(xl + m);
-                    });
-                    const int64_t jb = coop_count(0, lane, [&](int64_t m) {
-                        return sta - 1 - m >= 0 && xl - 1 - m >= done && P.b(sta - 1 - m) == P.b(xl - 1 - m);
-                    });
-                    ista = xl - jb;
-                    ienda = xl + jf;
-                }
+
+            // -- hash inserts of the visited lanes 0..last, last writer wins (writer.go:216-217)
+            const int last = a < 0 ? nvalid - 1 : a;
+            if (valid && lane <= last && next > last) {
+                ht[h] = (uint32_t)(start + x);
+                if (usefp) fp[h] = cur;
             }
-            break;
-        }
+            if (valid) bmask[bk] = 0;
+            __syncthreads();
 
-        // -- hash inserts of the visited lanes 0..last, last writer wins (writer.go:216-217)
-        const int last = a < 0 ? nvalid - 1 : a;
-        if (valid && lane <= last && next > last) {
-            ht[h] = (uint32_t)(start + x);
-            if (usefp) fp[h] = cur;
-        }
-        if (valid) bmask[bk] = 0;
-        __syncthreads();
+            if (a < 0) { i += nvalid; continue; }
 
-        if (a < 0) { i += nvalid; continue; }
-
-        // -- lane a's action
-        if (ka == kWin) {
-            // writer.go:303-321
-            if (done < ista) put_literal(o, P, done, ista, lane);
-            const int64_t dist = start + xa - canda;  // w.pos - st after the literal
-            const int64_t L = ienda - ista;
-            if (dist > bs) { o.err = EZ_EINVAL; break; }  // panic("too big offset")
-            Hdr hh;
-            if (!hdr_tag(hh, kCopy, L) || !hdr_offset(hh, dist, L)) { o.err = EZ_EINVAL; break; }
-            put_hdr(o, hh, lane);
-            if (xa + 1 + 4 <= n) {
-                const uint32_t h1 = (P.u32(xa + 1) * kHashMul) >> hsh;
-                V16 c1{0, 0};
-                if (usefp) {
-                    const int src = a + 1 < kWave ? a + 1 : a;
-                    c1 = V16{(uint64_t)__shfl((long long)cur.lo, src, 64), (uint64_t)__shfl((long long)cur.hi, src, 64)};
-                    if (a + 1 >= kWave) c1 = around(xa + 1);
-                }
-                if (lane == 0) {
-                    ht[h1] = (uint32_t)(start + xa + 1);
-                    if (usefp) fp[h1] = c1;
-                }
-                __syncthreads();
-            }
-            i = ienda;
-            done = ienda;
-        } else if (ka == kRun) {
-            // writer.go:477-488 (the literal is unconditional: SURVEY A.6)
-            put_literal(o, P, done, ista, lane);
-            Hdr hh;
-            if (!hdr_tag(hh, kCopy, ienda - ista) || !hdr_offset(hh, xa - sta, ienda - ista)) { o.err = EZ_EINVAL; break; }
-            put_hdr(o, hh, lane);
-            i = ienda;
-            done = ienda;
-        } else if (ka == kCut) {
-            // writer.go:464-473
-            const int64_t iend = done + xa - sta;
-            put_literal(o, P, done, iend, lane);
-            i = iend;
-            done = iend;
-        } else {
-            // writeZeros writer.go:407-439, called with i = st
-            const int64_t zf = coop_count(0, lane, [&](int64_t m) { return sta + m < n && P.b(sta + m) == 0; });
-            const int64_t zb = coop_count(0, lane, [&](int64_t m) { return sta - 1 - m >= done && P.b(sta - 1 - m) == 0; });
-            const int64_t zi = sta - zb, ziend = sta + zf;
-            if (ziend - zi < kMinCopyChunk) {
-                i = zi + 1;  // unreachable: >= 8 zeros are guaranteed
-            } else {
-                if (done != zi) put_literal(o, P, done, zi, lane);
+            // -- lane a's action
+            if (ka == kWin) {
+                // writer.go:303-321
+                if (done < ista) put_literal(o, P, done, ista, lane);
+                const int64_t dist = start + xa - canda;  // w.pos - st after the literal
+                const int64_t L = ienda - ista;
+                if (dist > bs) { o.err = EZ_EINVAL; break; }  // panic("too big offset")
                 Hdr hh;
-                if (!hdr_tag(hh, kCopy, ziend - zi)) { o.err = EZ_EINVAL; break; }
-                hh.put(kOffLong);
-                hh.put(0);
+                if (!hdr_tag(hh, kCopy, L) || !hdr_offset(hh, dist, L)) { o.err = EZ_EINVAL; break; }
                 put_hdr(o, hh, lane);
-                i = ziend;
-                done = ziend;
+                if (xa + 1 + 4 <= n) {
+                    const uint32_t h1 = (P.u32(xa + 1) * kHashMul) >> hsh;
+                    V16 c1{0, 0};
+                    if (usefp) {
+                        const int src = a + 1 < kWave ? a + 1 : a;
+                        c1 = V16{(uint64_t)__shfl((long long)cur.lo, src, 64), (uint64_t)__shfl((long long)cur.hi, src, 64)};
+                        if (a + 1 >= kWave) c1 = around(xa + 1);
+                    }
+                    if (lane == 0) {
+                        ht[h1] = (uint32_t)(start + xa + 1);
+                        if (usefp) fp[h1] = c1;
+                    }
+                    __syncthreads();
+                }
+                i = ienda;
+                done = ienda;
+            } else if (ka == kRun) {
+                // writer.go:477-488 (the literal is unconditional: SURVEY A.6)
+                put_literal(o, P, done, ista, lane);
+                Hdr hh;
+                if (!hdr_tag(hh, kCopy, ienda - ista) || !hdr_offset(hh, xa - sta, ienda - ista)) { o.err = EZ_EINVAL; break; }
+                put_hdr(o, hh, lane);
+                i = ienda;
+                done = ienda;
+            } else if (ka == kCut) {
+                // writer.go:464-473
+                const int64_t iend = done + xa - sta;
+                put_literal(o, P, done, iend, lane);
+                i = iend;
+                done = iend;
+            } else {
+                // writeZeros writer.go:407-439, called with i = st
+                const int64_t zf = coop_count(0, lane, [&](int64_t m) { return sta + m < n && P.b(sta + m) == 0; });
+                const int64_t zb = coop_count(0, lane, [&](int64_t m) { return sta - 1 - m >= done && P.b(sta - 1 - m) == 0; });
+                const int64_t zi = sta - zb, ziend = sta + zf;
+                if (ziend - zi < kMinCopyChunk) {
+                    i = zi + 1;  // unreachable: >= 8 zeros are guaranteed
+                } else {
+                    if (done != zi) put_literal(o, P, done, zi, lane);
+                    Hdr hh;
+                    if (!hdr_tag(hh, kCopy, ziend - zi)) { o.err = EZ_EINVAL; break; }
+                    hh.put(kOffLong);
+                    hh.put(0);
+                    put_hdr(o, hh, lane);
+                    i = ziend;
+                    done = ziend;
+                }
             }
         }
-    }
-    // trailing literal (writer.go:324-329)
-    if (!o.err && done < n) put_literal(o, P, done, n, lane);
+        // trailing literal (writer.go:324-329)
+        if (!o.err && done < n) put_literal(o, P, done, n, lane);
 
+        if (!mw || ++wk >= wlast || o.err) break;
+        // the next Write: its bytes follow this one's in the batch
+        start += n;
+        wbeg = A.write_end[wk - 1];
+        n = (int64_t)(A.write_end[wk] - wbeg);
+        P.g = A.in + wbeg;
+        P.gr = (uint64_t)(uintptr_t)P.g & 3;
+        P.gw = (const uint32_t *)(P.g - P.gr);
+        P.glast = (P.gr + (uint64_t)n + 3) / 4;
+        P.glast = P.glast ? P.glast - 1 : 0;
+    }
     if (RING) {
         // copyData of this Write into the ring (writer.go:529-535), and
         // the hash table back to HBM.
@@ -560,7 +583,7 @@ hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;
     if (compress_variant(a) == 's') return launch_compress_split(a, a.ht_global, st);
     const bool htl = a.hs <= kHtLdsMax;
-    const bool pl = a.max_len > 0 && (int64_t)a.max_len <= kPLdsMax;
+    const bool pl = a.max_len > 0 && (int64_t)a.max_len <= kPLdsMax && !a.write_idx;  // multi-Write: the global view
     const bool ring = a.ring != nullptr;
     size_t lds = (htl ? (size_t)a.hs * 4 : 0) + kMaskBytes + kHashBytes;
     if (pl) lds += ((a.max_len + 3) / 4 + 8) * 4;

@@ -183,6 +183,22 @@ struct Pred<0, ROW> {
     __device__ __forceinline__ static int32_t get(uint32_t, int, int32_t d) { return d; }
 };
 
+// The same search on hashes offset to be nonzero, with DPP bound_ctrl (a lane K below outside the
+// row reads 0, which never equals): the shifted read can fold into the compare (no v_mov of the
+// row-edge default per step)
+template <int K>
+struct PredZ {
+    __device__ __forceinline__ static int32_t get(uint32_t hp, int32_t d) {
+        const uint32_t hk = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)hp, 0x110 + K, 0xf, 0xf, true);
+        d = hk == hp ? K : d;  // descending K: the nearest one stays
+        return PredZ<K - 1>::get(hp, d);
+    }
+};
+template <>
+struct PredZ<0> {
+    __device__ __forceinline__ static int32_t get(uint32_t, int32_t d) { return d; }
+};
+
 // ---------------------------------------------------------------- K1p
 // GIN: stream bytes read through L1/L2 (GW); else staged in LDS after the table (PW)
 // MW: streams of several Writes (CompressArgs::write_idx), else one Write each
@@ -445,9 +461,17 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
 // Loads of the lean parse carry no bounds logic: every stream the loop reads has 16 readable bytes
 // before it and 64 after it (k1_lean copies the few streams at the batch's edges into padded
 // slots first), so each piece is one plain aligned load.
+// (global address space: plain global_load instructions, not flat ones, which would also count
+// against the LDS counter and wait on the ds_bpermute traffic)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef const __attribute__((address_space(1))) uint32_t *gu32p;
+typedef const __attribute__((address_space(1))) u32x4 *gu128p;
 struct LeanIn {
-    __device__ __forceinline__ uint32_t dw(const uint8_t *w) const { return *(const uint32_t *)w; }
-    __device__ __forceinline__ uint4 dw4(const uint8_t *w) const { return *(const uint4 *)w; }
+    __device__ __forceinline__ uint32_t dw(const uint8_t *w) const { return *(gu32p)w; }
+    __device__ __forceinline__ uint4 dw4(const uint8_t *w) const {
+        const u32x4 v = *(gu128p)w;
+        return make_uint4(v.x, v.y, v.z, v.w);
+    }
 };
 // gext's view of a padded stream: GW::around without the batch-bounds branch (bytes before the
 // stream start read 0; gext reads at most 16 bytes before it and 16 after its end)
@@ -498,6 +522,29 @@ struct WinDw {
 // and v_alignbyte: a 16-byte load at a byte-unaligned address costs the L1 one access per dword it
 // touches, an aligned one a single access (tools/mb_ta.hip, L1-resident: 64 vs 16 ns per scattered
 // wave-load), so this is 3 accesses per lane instead of ~8.
+// The candidate's 28 bytes y-8 .. y+19 from two dword-aligned 16-byte loads (floor4(p + y - 8)),
+// for a forward cap of 20 instead of 24 (EZ_EXP & 8 builds, A/B: one load fewer per lane, more
+// matches taking gext)
+#if (EZ_EXP & 8)
+constexpr int32_t kFwdCap = 20;
+#else
+constexpr int32_t kFwdCap = 24;
+#endif
+__device__ __forceinline__ void bytes28(const LeanIn &L, const uint8_t *p, int32_t y, V16 &c0, V16 &c1) {
+    const uintptr_t a = (uintptr_t)(p + y - 8);
+    const uint32_t r = (uint32_t)(a & 3);
+    const uint8_t *w = (const uint8_t *)(a & ~(uintptr_t)3);
+    const uint4 q0 = L.dw4(w), q1 = L.dw4(w + 16);
+    const uint32_t d[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+    uint32_t b[7];
+#pragma unroll
+    for (int t = 0; t < 7; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+    c0.lo = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+    c0.hi = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
+    c1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
+    c1.hi = (uint64_t)b[6];
+}
+
 __device__ __forceinline__ void bytes32(const LeanIn &L, const uint8_t *p, int32_t y, V16 &c0, V16 &c1) {
     const uintptr_t a = (uintptr_t)(p + y - 8);
     const uint32_t r = (uint32_t)(a & 3);
@@ -512,6 +559,44 @@ __device__ __forceinline__ void bytes32(const LeanIn &L, const uint8_t *p, int32
     c0.hi = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
     c1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
     c1.hi = (uint64_t)b[6] | ((uint64_t)b[7] << 32);
+}
+
+// Byte counts without branches: v_ffbl / v_ffbh return ~0u for 0, and saturating adds keep that
+// "no bit here" through the word offsets, so a min over the words finds the first set bit.
+__device__ __forceinline__ uint32_t ffbl32(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ uint32_t ffbh32(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbh_u32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ uint32_t sat_add(uint32_t a, uint32_t b) { return __builtin_elementwise_add_sat(a, b); }
+// equal leading (low-address) bytes of the 24 bytes whose xor is (e0, e1, e2): 0 .. 24
+__device__ __forceinline__ int32_t first_diff24(uint64_t e0, uint64_t e1, uint64_t e2) {
+    uint32_t m = ffbl32((uint32_t)e0);
+    m = min(m, sat_add(ffbl32((uint32_t)(e0 >> 32)), 32u));
+    m = min(m, sat_add(ffbl32((uint32_t)e1), 64u));
+    m = min(m, sat_add(ffbl32((uint32_t)(e1 >> 32)), 96u));
+    m = min(m, sat_add(ffbl32((uint32_t)e2), 128u));
+    m = min(m, sat_add(ffbl32((uint32_t)(e2 >> 32)), 160u));
+    return (int32_t)min(m >> 3, 24u);
+}
+// the same over 20 bytes (e2: the last 4): 0 .. 20
+__device__ __forceinline__ int32_t first_diff20(uint64_t e0, uint64_t e1, uint32_t e2) {
+    uint32_t m = ffbl32((uint32_t)e0);
+    m = min(m, sat_add(ffbl32((uint32_t)(e0 >> 32)), 32u));
+    m = min(m, sat_add(ffbl32((uint32_t)e1), 64u));
+    m = min(m, sat_add(ffbl32((uint32_t)(e1 >> 32)), 96u));
+    m = min(m, sat_add(ffbl32(e2), 128u));
+    return (int32_t)min(m >> 3, 20u);
+}
+// equal trailing (high-address) bytes of the 8 bytes whose xor is e: 0 .. 8
+__device__ __forceinline__ int32_t last_diff8(uint64_t e) {
+    const uint32_t m = min(ffbh32((uint32_t)(e >> 32)), sat_add(ffbh32((uint32_t)e), 32u));
+    return (int32_t)min(m >> 3, 8u);
 }
 
 __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int32_t n, int lj, int g, uint16_t *hth,
@@ -541,11 +626,12 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         if (prio & 1) __builtin_amdgcn_s_setprio(3);
         const uint32_t h = valid ? ((uint32_t)w0.hi * kHashMul) >> hsh : 0u;
         const int32_t tv = valid ? (int32_t)hth[h] : 0;
-        const int32_t d = Pred<G - 1, true>::get(h, lj, 0);
+        const int32_t d = PredZ<G - 1>::get(valid ? h + 1 : 0u, 0);
         const int32_t cand = valid ? (d ? x - d : tv) : 0;
         V16 c0 = z0, c1 = z1;
         if (cand != 0) {
-            bytes32(L, p, cand, c0, c1);
+            if (kFwdCap == 20) bytes28(L, p, cand, c0, c1);
+            else bytes32(L, p, cand, c0, c1);
             // bytes before the stream start are the fresh ring's zeros
             c0.lo &= cand >= 8 ? ~0ull : ~0ull << (8 * (8 - cand));
         }
@@ -554,11 +640,11 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         // ---- capped judgement, writer.go:219-301 (window) and :441-463 (writeRunlen)
         const bool rl = cand >= done && cand < x;
         const uint64_t e0 = w0.hi ^ c0.hi, e1 = w1.lo ^ c1.lo, e2 = w1.hi ^ c1.hi;
-        int32_t jf = e0 ? ctz_bytes(e0) : (e1 ? 8 + ctz_bytes(e1) : 16 + ctz_bytes(e2));
+        int32_t jf = kFwdCap == 20 ? first_diff20(e0, e1, (uint32_t)e2) : first_diff24(e0, e1, e2);
         jf = jf < n - x ? jf : n - x;
         int32_t bl = x - done;
         if (rl) bl = bl < cand ? bl : cand;
-        int32_t jb = clz_bytes(w0.lo ^ c0.lo);
+        int32_t jb = last_diff8(w0.lo ^ c0.lo);
         jb = jb < bl ? jb : bl;
         const bool zr = rl && c0.hi == 0 && cand + 8 < n;
         const int32_t fw = rl ? jf : (jf < done - cand ? jf : done - cand);
@@ -568,20 +654,21 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         int32_t lit, nx, dist, ext;
         bool force = false;
         if (zr) {  // writeZeros :407-439
-            int32_t zf = 8 + (c1.lo ? ctz_bytes(c1.lo) : 8 + ctz_bytes(c1.hi));
+            int32_t zf = kFwdCap == 20 ? first_diff20(0, c1.lo, (uint32_t)c1.hi) : first_diff24(0, c1.lo, c1.hi);
             zf = zf < n - cand ? zf : n - cand;
-            int32_t zb = clz_bytes(c0.lo);
+            int32_t zb = last_diff8(c0.lo);
             zb = zb < cand - done ? zb : cand - done;
             lit = cand - zb;
             nx = cand + zf;
             dist = 0;
-            ext = (zf == 24 && n - cand > 24 ? 1 : 0) | (zb == 8 && cand - done > 8 ? 2 : 0);
+            ext = (zf == kFwdCap && n - cand > kFwdCap ? 1 : 0) | (zb == 8 && cand - done > 8 ? 2 : 0);
         } else {  // writeRunlen :441-489 / window match :303-321
             lit = x - jb;
             nx = x + fw;
             dist = x - cand;
             force = rl;
-            ext = (jf == 24 && (rl ? n - x : (done - cand < n - x ? done - cand : n - x)) > 24 ? 1 : 0) | (jb == 8 && bl > 8 ? 2 : 0);
+            ext = (jf == kFwdCap && (rl ? n - x : (done - cand < n - x ? done - cand : n - x)) > kFwdCap ? 1 : 0) |
+                  (jb == 8 && bl > 8 ? 2 : 0);
         }
         const uint64_t am64 = __ballot(acc);
         const uint32_t am = (uint32_t)(am64 >> (G * g)) & 0xffffu;
@@ -613,7 +700,7 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
             const int32_t blim = zra ? ca - done : (rla ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
             const int32_t flim = zra ? n - ca : (rla ? n - xa : ((done - ca) < n - xa ? done - ca : n - xa));
             int32_t fx, cx;
-            gext<G, GWU>(GWU{p}, need && (e & 1), need && (e & 2), g, lj, fa, ca, mode, done, 24, flim, blim, fx, cx);
+            gext<G, GWU>(GWU{p}, need && (e & 1), need && (e & 2), g, lj, fa, ca, mode, done, kFwdCap, flim, blim, fx, cx);
             if (need) {
                 const int32_t f = (e & 1) ? fx : (sel & 0x0fffffff) - fa;
                 const int32_t c = (e & 2) ? cx : ((ib >> 16) & 0xf);
@@ -913,7 +1000,9 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     hipError_t z = hipMemsetAsync(edge, 0, 128, st);
     if (z == hipSuccess) z = hipMemsetAsync(edge + 128 + kEdgeSlots * edge_slot_bytes(a), 0, 16, st);
     if (z != hipSuccess) return z;
-    hipLaunchKernelGGL(k1_lean, dim3(grid), dim3(64), (size_t)stride * 4 * S, st, a, stride, tw, recs, rcap, prio, edge);
+    // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
+    static const size_t pad = getenv("EZ_K1S_LDSPAD") ? (size_t)atoi(getenv("EZ_K1S_LDSPAD")) : 0;
+    hipLaunchKernelGGL(k1_lean, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);

@@ -103,6 +103,10 @@ int ez_writer_break(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n);  /* 
 int ez_writer_reset(ez_writer *w);                                          /* Reset       writer.go:149 (reset :187) */
 int ez_writer_reset_size(ez_writer *w, int64_t block, int64_t htable);     /* ResetSize   writer.go:155 */
 int ez_writer_is_reset(const ez_writer *w);                                 /* isreset     writer.go:403 */
+/* Testing hook (no reference counterpart): set w.pos, ring and table unchanged, so a test can
+ * run Writes across stream position 2^32, where the table's uint32 values (writer.go:216-217)
+ * stop matching; the C oracle has the same hook. */
+int ez_writer_set_position(ez_writer *w, int64_t pos);
 
 /* ---- streaming Reader handle: the decoder state of reader.go Reader (:17-40) ----
  * Window, position and current token live on the device.  The host shim owns
@@ -148,8 +152,8 @@ int ez_compress_batch(int64_t block, int64_t htable, int flags, const ez_batch *
  * k = write_idx[s] .. write_idx[s+1]-1 (device arrays, write_idx[count+1]);
  * Write k is in[prev .. write_end[k]) with prev = in_off[s] for the first.
  * max_writes: the most Writes of one stream (host hint).  Slots need
- * ez_compress_bound(n) + 5 bytes per Write.  Fresh streams with 2 x length
- * <= block only (the K1s regime); otherwise EZ_EINVAL. */
+ * ez_compress_bound(n) + 5 bytes per Write.  Streams of any length: K1s takes
+ * batches with 2 x length <= block, the general kernel the others. */
 int ez_compress_batch_writes(int64_t block, int64_t htable, int flags, const ez_batch *b, const uint64_t *write_idx,
                              const uint64_t *write_end, uint64_t max_writes, void *hip_stream);
 /* K3: exclusive scan of sizes -> packed_off[count+1], then gather the slots

@@ -526,6 +526,9 @@ const uint8_t *or_writer_sink(const or_writer *w, int64_t *len) { *len = w->sink
 void or_writer_sink_clear(or_writer *w) { w->sink.len = 0; }
 int64_t or_writer_sink_writes(const or_writer *w) { return w->sink_writes; }
 int64_t or_writer_pos(const or_writer *w) { return w->pos; }
+/* testing hook: the stream position (w.pos) of a writer, ring and table unchanged; lets a test
+   reach positions past 2^32 (the uint32 table values of writer.go:216-217) */
+void or_writer_set_pos(or_writer *w, int64_t pos) { w->pos = pos; }
 
 /* ---------------------------------------------------------------- Reader */
 

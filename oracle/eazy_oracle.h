@@ -71,6 +71,7 @@ const uint8_t *or_writer_sink(const or_writer *w, int64_t *len);
 void or_writer_sink_clear(or_writer *w);
 int64_t or_writer_sink_writes(const or_writer *w);
 int64_t or_writer_pos(const or_writer *w);
+void or_writer_set_pos(or_writer *w, int64_t pos); /* testing hook */
 
 /* ---- Reader (reader.go:17-543) ---- */
 typedef struct or_reader or_reader;

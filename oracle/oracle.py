@@ -54,6 +54,7 @@ def lib():
         L.or_writer_sink_clear.argtypes = [C.c_void_p]
         L.or_writer_pos.restype = _i64
         L.or_writer_pos.argtypes = [C.c_void_p]
+        L.or_writer_set_pos.argtypes = [C.c_void_p, _i64]
         L.or_reader_new_bytes.restype = C.c_void_p
         L.or_reader_new_bytes.argtypes = [C.c_char_p, _i64]
         L.or_reader_new.restype = C.c_void_p
@@ -177,6 +178,9 @@ class Writer:
     @property
     def pos(self):
         return lib().or_writer_pos(self._w)
+
+    def set_pos(self, pos: int) -> None:  # testing hook
+        lib().or_writer_set_pos(self._w, pos)
 
 
 class Reader:

@@ -166,16 +166,43 @@ def test_split_kernel_selected(cuda, k1_kind):
     assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) == "w"  # 2n > block: only the general kernel
 
 
+def _multi_write_check(cuda, streams, block=MiB, htable=1024):
+    """streams: lists of Writes; the slot of each equals the oracle's sink bytes."""
+    import torch
+
+    import eazy_amd as ez
+
+    data = b"".join(b"".join(ws) for ws in streams)
+    in_off, w_idx, w_end = [0], [0], []
+    pos = 0
+    for ws in streams:
+        for w in ws:
+            pos += len(w)
+            w_end.append(pos)
+        in_off.append(pos)
+        w_idx.append(len(w_end))
+    t = lambda a: torch.tensor(a, dtype=torch.int64, device=cuda)
+    host = np.frombuffer(data, np.uint8)
+    dd = torch.from_numpy(host.copy()).to(cuda) if len(host) else torch.zeros(1, dtype=torch.uint8, device=cuda)
+    cb = ez.compress_batch_writes(dd, t(in_off), t(w_idx), t(w_end), block, htable)
+    torch.cuda.synchronize()
+    st, sz, so = cb.status.cpu().numpy(), cb.sizes.cpu().numpy(), cb.slot_off.cpu().numpy()
+    slots = cb.slots.cpu().numpy()
+    for s, ws in enumerate(streams):
+        assert st[s] == 0, (s, st[s])
+        want = orc.compress(block, htable, ws)
+        got = slots[so[s] : so[s] + sz[s]].tobytes()
+        assert got == want, f"stream {s}: {len(ws)} Writes of {[len(w) for w in ws]}"
+
+
 def test_multi_write_streams(cuda, k1_kind):
     """Streams that each receive several Writes (one NewWriter, k calls of
     Write, FlushThreshold 0): the slot holds the bytes the sink
     receives over the k calls, equal to the oracle's for the same Writes —
-    ragged Writes, empty ones, ones shorter than a hash (4 bytes), one Write."""
-    if k1_kind:
-        pytest.skip("multi-Write batches run on the automatic K1s choice")
-    import torch
-
-    import eazy_amd as ez
+    ragged Writes, empty ones, ones shorter than a hash (4 bytes), one Write.
+    K1s takes these (2 x length <= block); forced 'w' runs the general kernel."""
+    if k1_kind == "S":
+        pytest.skip("the u32-table K1s is covered by the automatic choice's long streams")
     from eazy_amd import synth
 
     rng = np.random.default_rng(21)
@@ -189,28 +216,33 @@ def test_multi_write_streams(cuda, k1_kind):
             ws.append(d[at : at + n])
             at += n
         streams.append(ws)
-    data = b"".join(b"".join(ws) for ws in streams)
-    in_off, w_idx, w_end = [0], [0], []
-    pos = 0
-    for ws in streams:
-        for w in ws:
-            pos += len(w)
-            w_end.append(pos)
-        in_off.append(pos)
-        w_idx.append(len(w_end))
-    dev = cuda
-    t = lambda a: torch.tensor(a, dtype=torch.int64, device=dev)
-    host = np.frombuffer(data, np.uint8)
-    dd = torch.from_numpy(host.copy()).to(dev) if len(host) else torch.zeros(1, dtype=torch.uint8, device=dev)
-    cb = ez.compress_batch_writes(dd, t(in_off), t(w_idx), t(w_end), MiB, 1024)
-    torch.cuda.synchronize()
-    st, sz, so = cb.status.cpu().numpy(), cb.sizes.cpu().numpy(), cb.slot_off.cpu().numpy()
-    slots = cb.slots.cpu().numpy()
-    for s, ws in enumerate(streams):
-        assert st[s] == 0, (s, st[s])
-        want = orc.compress(MiB, 1024, ws)
-        got = slots[so[s] : so[s] + sz[s]].tobytes()
-        assert got == want, f"stream {s}: {len(ws)} Writes of {[len(w) for w in ws]}"
+    _multi_write_check(cuda, streams)
+
+
+def test_multi_write_streams_beyond_half_window(cuda, k1_kind):
+    """Multi-Write streams longer than half the window run on the general kernel: the
+    history of earlier Writes is read across Write boundaries, the ring wraps (block 4096 /
+    32 KiB with Writes of up to 3 KiB / 40 KiB), far skips and the cut branch occur, and a
+    1 MiB window with 3 x 400 KiB log Writes (writer.go:206-217, 280-296)."""
+    if k1_kind:
+        pytest.skip("one K1 choice suffices: these batches only fit the general kernel")
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    assert ez.compress_kernel(4096, 64, 9000, 40) == "w"
+    rng = np.random.default_rng(31)
+    d = synth.logs(33, 4 << 20).tobytes()
+    streams, at = [], 0
+    for s in range(40):
+        ws = []
+        for _ in range(int(rng.integers(2, 6))):
+            n = int(rng.integers(0, 3000))
+            ws.append(d[at : at + n] if s % 3 else rng.integers(0, 4, n, dtype=np.uint8).tobytes())
+            at += n
+        streams.append(ws)
+    _multi_write_check(cuda, streams, block=4096, htable=64)
+    _multi_write_check(cuda, [[d[k * 40000 : (k + 1) * 40000] for k in range(j, j + 4)] for j in range(6)], block=1 << 15, htable=256)
+    _multi_write_check(cuda, [[d[:409600], d[409600:819200], d[819200:1228800]], [d[2 << 20 :(2 << 20) + 700000], b"", d[:5000]]])
 
 
 def test_sub_batches_through_offset_views(cuda):

@@ -319,3 +319,38 @@ def test_reader_large_stream_small_reads(cuda):
             break
         assert err == ez.OK, err
     assert bytes(out) == plain
+
+
+def test_writer_positions_past_4gib(cuda):
+    """A Writer whose position crosses 2^32 (the table holds uint32(start + i),
+    writer.go:216-217, so entries written past 2^32 look far away and are skipped): the handle's
+    bytes equal the oracle's from the same state (testing hook on both: w.pos set, zero ring
+    and table)."""
+    import ctypes as C
+
+    import eazy_amd as ez
+    import oracle as orc
+    from eazy_amd import synth
+
+    d = synth.logs(71, 16 * 4096).tobytes()
+    writes = [d[k * 4096 : (k + 1) * 4096] for k in range(16)]
+    for p0 in ((1 << 32) - 10000, (1 << 32) - 1, (1 << 33) + 5):
+        ow = orc.Writer(1 << 20, 1024)
+        ow.set_pos(p0)
+        for w in writes:
+            ow.write(w)
+        L = ez._lib()
+        L.ez_writer_set_position.argtypes = [C.c_void_p, C.c_int64]
+        h = C.c_void_p()
+        assert L.ez_writer_new(1 << 20, 1024, 0, C.byref(h)) == 0
+        try:
+            assert L.ez_writer_set_position(h, p0) == 0
+            outs, n = [], C.c_size_t()
+            for w in writes:
+                cap = ez.compress_bound(len(w))
+                buf = (C.c_uint8 * cap)()
+                assert L.ez_writer_write(h, w, len(w), buf, cap, C.byref(n)) == 0
+                outs.append(bytes(buf[: n.value]))
+        finally:
+            L.ez_writer_free(h)
+        assert b"".join(outs) == ow.sink, f"p0 = {p0:#x}"

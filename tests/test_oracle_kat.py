@@ -43,3 +43,22 @@ def test_writer_panics():
             orc.Writer(bs, hs)
         with pytest.raises(py.Panic):
             py.Writer(bs, hs)
+
+
+def test_oracle_uint32_position_wrap():
+    """SURVEY A.9 on the oracle: a Writer at 2^32 - 10000 loses the matches whose table
+    entries were written past 2^32 (uint32 values look ~4 GiB away: far skip), so the same
+    Writes compress worse than from position 0; at 2^25 nothing changes."""
+    from eazy_amd import synth
+
+    d = synth.logs(71, 16 * 4096).tobytes()
+    writes = [d[k * 4096 : (k + 1) * 4096] for k in range(16)]
+    out = {}
+    for p0 in (0, 1 << 25, (1 << 32) - 10000):
+        w = orc.Writer(1 << 20, 1024)
+        w.set_pos(p0)
+        for p in writes:
+            w.write(p)
+        out[p0] = w.sink
+    assert out[0] == out[1 << 25]
+    assert len(out[(1 << 32) - 10000]) > 1.5 * len(out[0])
