@@ -477,15 +477,6 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # correctness of this run: statuses, sizes and the full round trip on device
-    if not args.no_check:
-        assert int(cb.status.abs().sum()) == 0, "compress status"
-        assert int(ost.abs().sum()) == 0, "decompress status"
-        assert bool(torch.equal(out[:total], data)), "round trip differs"
-        if sharded:
-            base = int(goff[0][first_all[rank]])
-            assert torch.equal(goff[0][first_all[rank] : first_all[rank + 1] + 1] - base, poff), "global offsets"
-    comp_bytes = int(poff[-1])
 
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(args.steps)]
     ezd.barrier(R)
@@ -501,6 +492,15 @@ def main():
     k3 = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
     xch = sum(e[2].elapsed_time(e[3]) for e in evs) / args.steps
     k2 = sum(e[3].elapsed_time(e[4]) for e in evs) / args.steps
+    # correctness of the timed steps' results: statuses, sizes and the full round trip on device
+    if not args.no_check:
+        assert int(cb.status.abs().sum()) == 0, "compress status"
+        assert int(ost.abs().sum()) == 0, "decompress status"
+        assert bool(torch.equal(out[:total], data)), "round trip differs"
+        if sharded:
+            base = int(goff[0][first_all[rank]])
+            assert torch.equal(goff[0][first_all[rank] : first_all[rank + 1] + 1] - base, poff), "global offsets"
+    comp_bytes = int(poff[-1])
     elapsed, k1, k2, k3, xch = ezd.reduce_max([elapsed, k1, k2, k3, xch], R, dev)  # the job ends with its slowest rank
     (comp_all,) = ezd.reduce_sum([comp_bytes], R, dev)
 

@@ -130,7 +130,8 @@ def device_count() -> int:
 
 def compress_kernel(block: int, htable: int, max_len: int, count: int) -> str:
     """The K1 kernel a batch of `count` fresh streams of <= max_len bytes runs
-    on the current device ('s' K1s: parse + token writer, 'w' general wave per stream)."""
+    on the current device ('s' K1s: parse + token writer, 'x' K1x's data-parallel rounds
+    then the general kernel, 'w' general wave per stream)."""
     L = _lib()
     L.ez_compress_kernel.argtypes = [C.c_int64, C.c_int64, C.c_uint64, C.c_uint64]
     v = L.ez_compress_kernel(block, htable, max_len, count)
@@ -141,7 +142,8 @@ def compress_kernel(block: int, htable: int, max_len: int, count: int) -> str:
 
 def select_compress_kernel(kind: str = "") -> None:
     """Force the K1 kernel of later batch calls ('s' K1s, 'S' K1s with the u32
-    exchange table, 'w' general; '' = automatic).  Tests and A/B measurement only."""
+    exchange table, 'w' general alone, 'x' K1x's rounds for any fresh single-Write batch;
+    '' = automatic).  Tests and A/B measurement only."""
     _check(_lib().ez_select_compress_kernel(ord(kind) if kind else 0))
 
 

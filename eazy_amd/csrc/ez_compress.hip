@@ -177,8 +177,11 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         if (lane < 4) lw[nw + lane] = 0;
     }
     // ---- hash table and bucket masks
+    // K1x resume: the table K1x prepared (spec_mode 1: at its first emitting position; 2: at from)
+    const int smode = RING ? 0 : A.spec_mode;
     if (HTL) {
         if (RING) for (int64_t k = lane; k < hs; k += kWave) ht[k] = A.ht_global[k];
+        else if (smode) for (int64_t k = lane; k < hs; k += kWave) ht[k] = A.spec_tab[s * (uint64_t)hs + k];
         else for (int64_t k = lane; k < hs; k += kWave) ht[k] = 0;
     } else if (!RING) {
         for (int64_t k = lane; k < hs; k += kWave) ht[k] = 0;
@@ -189,11 +192,11 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     OutBuf o;
     o.p = A.out + A.out_off[s];
     o.cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
-    o.op = 0;
+    o.op = smode ? (int64_t)A.spec[s].op : 0;
     o.err = 0;
 
-    // ---- header (writer.go:207-209, 495-517)
-    if (A.header) {
+    // ---- header (writer.go:207-209, 495-517; K1x wrote it for the streams it resumes)
+    if (A.header && !smode) {
         Hdr h;
         if (A.append_magic) { h.put(0x80); h.put(0x02); h.put('e'); h.put('a'); h.put('z'); h.put('y'); }
         if (A.ver != 0) { h.put(0x80); h.put(0x08); h.put((uint32_t)A.ver); }
@@ -228,8 +231,22 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         return false;
     };
 
+    // appendLiteral; in spec_mode 1 the bytes are left to K1x's copy kernel (a literal there can be
+    // megabytes, one wave would copy it at 1 KiB per step)
+    auto literal = [&](int64_t st, int64_t end) {
+        if (smode != 1) { put_literal(o, P, st, end, lane); return; }
+        Hdr h;
+        if (!hdr_tag(h, kLiteral, end - st)) { o.err = EZ_EINVAL; return; }
+        put_hdr(o, h, lane);
+        if (o.err) return;
+        if (o.op + (end - st) > o.cap) { o.err = EZ_ENOSPC; return; }
+        if (lane == 0 && end > st) A.spec_lit[atomicAdd(A.spec_nlit, 1u)] = SpecLit{ib + (uint64_t)st, A.out_off[s] + (uint64_t)o.op, (uint64_t)(end - st)};
+        o.op += end - st;
+    };
+    bool stopped = false;  // spec_mode 1: stopped after one accepted copy
     for (;;) {  // the stream's Writes (one unless mw)
-        int64_t done = 0, i = 0;
+        int64_t done = smode ? (int64_t)A.spec[s].done : 0;
+        int64_t i = smode == 1 ? (int64_t)A.spec_first[s] : (smode == 2 ? (int64_t)A.spec[s].from : 0);
         int64_t guard = 0;
         const int64_t guard_max = 16 * n + 4096;
         // global input: the 16 bytes x-8 .. x+7 around each lane's position, and those of
@@ -241,7 +258,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         };
         V16 nxt_w{0, 0};
         int64_t nxt_i = -1;
-        const bool usefp = FP && pf && start == 0;
+        const bool usefp = FP && pf && start == 0 && !smode;
         if (usefp) {  // the zero entries hold stream position 0
             const V16 z = around(0);
             for (int64_t k = lane; k < hs; k += kWave) fp[k] = z;
@@ -448,7 +465,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
             // -- lane a's action
             if (ka == kWin) {
                 // writer.go:303-321
-                if (done < ista) put_literal(o, P, done, ista, lane);
+                if (done < ista) literal(done, ista);
                 const int64_t dist = start + xa - canda;  // w.pos - st after the literal
                 const int64_t L = ienda - ista;
                 if (dist > bs) { o.err = EZ_EINVAL; break; }  // panic("too big offset")
@@ -473,7 +490,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 done = ienda;
             } else if (ka == kRun) {
                 // writer.go:477-488 (the literal is unconditional: SURVEY A.6)
-                put_literal(o, P, done, ista, lane);
+                literal(done, ista);
                 Hdr hh;
                 if (!hdr_tag(hh, kCopy, ienda - ista) || !hdr_offset(hh, xa - sta, ienda - ista)) { o.err = EZ_EINVAL; break; }
                 put_hdr(o, hh, lane);
@@ -482,7 +499,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
             } else if (ka == kCut) {
                 // writer.go:464-473
                 const int64_t iend = done + xa - sta;
-                put_literal(o, P, done, iend, lane);
+                literal(done, iend);
                 i = iend;
                 done = iend;
             } else {
@@ -493,7 +510,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 if (ziend - zi < kMinCopyChunk) {
                     i = zi + 1;  // unreachable: >= 8 zeros are guaranteed
                 } else {
-                    if (done != zi) put_literal(o, P, done, zi, lane);
+                    if (done != zi) literal(done, zi);
                     Hdr hh;
                     if (!hdr_tag(hh, kCopy, ziend - zi)) { o.err = EZ_EINVAL; break; }
                     hh.put(kOffLong);
@@ -503,9 +520,19 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                     done = ziend;
                 }
             }
+            // spec_mode 1: one emitting position resolved; K1x speculates again from here
+            if (smode == 1 && i + 4 <= n && !o.err) {
+                stopped = true;
+                break;
+            }
+        }
+        if (stopped) {  // K1x's state back: the position, the pending literal, the output, the table
+            if (lane == 0) A.spec[s] = SpecState{(uint32_t)i, (uint32_t)done, (uint32_t)o.op, 0u};
+            if (HTL) for (int64_t k = lane; k < hs; k += kWave) A.spec_tab[s * (uint64_t)hs + k] = ht[k];
+            return;
         }
         // trailing literal (writer.go:324-329)
-        if (!o.err && done < n) put_literal(o, P, done, n, lane);
+        if (!o.err && done < n) literal(done, n);
 
         if (!mw || ++wk >= wlast || o.err) break;
         // the next Write: its bytes follow this one's in the batch
@@ -528,6 +555,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     if (lane == 0) {
         A.out_size[s] = (uint64_t)o.op;
         if (A.status) A.status[s] = o.err;
+        if (smode) A.spec[s].flags = 1u;  // finished
     }
 }
 
@@ -535,6 +563,8 @@ template <bool PL, bool HTL, bool RING>
 __global__ __launch_bounds__(64) void k1_compress(CompressArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     for (uint64_t s = blockIdx.x; s < A.count; s += gridDim.x) {
+        // K1x resumes: finished streams, and in mode 1 the ones without an emitting position
+        if (!RING && A.spec_mode && (A.spec[s].flags != 0 || (A.spec_mode == 1 && A.spec_first[s] == 0xffffffffu))) continue;
         compress_stream<PL, HTL, RING>(A, s, smem);
         __syncthreads();
     }
@@ -556,6 +586,7 @@ hipError_t launch_variant(const CompressArgs &a, hipStream_t st, size_t lds, uns
 uint64_t compress_scratch_words(const CompressArgs &a) {
     const char v = compress_variant(a);
     if (v == 's') return split_scratch_words(a);
+    if (v == 'x') return (spec_scratch_bytes(a) + 3) / 4;
     if (a.hs <= kHtLdsMax) return 0;
     const uint64_t grid = a.count < 2048 ? a.count : 2048;
     return grid * (uint64_t)a.hs;
@@ -564,8 +595,10 @@ uint64_t compress_scratch_words(const CompressArgs &a) {
 // K1 choice.  Fresh streams with 2n <= block and a table of at most 4096 entries take K1s
 // (ez_compress_split.hip: the parse kernel + the token writer); everything else -- writer handles
 // (rings), Writes longer than half the window (C4), large tables -- takes the general
-// wave-per-stream kernel below.  EZ_K1=general or ez_select_compress_kernel('w') forces the
-// general kernel (tests, A/B).
+// wave-per-stream kernel below, after K1x's rounds (ez_compress_spec.hip) for fresh single-Write
+// streams of 64 KiB and more.  EZ_K1=general or ez_select_compress_kernel('w') forces the general
+// kernel alone, 'x' K1x for any fresh single-Write batch with a table of at most 4096 entries
+// (tests, A/B).
 static int g_forced_variant = -1;  // -1: not read yet; 0: automatic; else the kernel's letter
 void select_compress_variant(int v) { g_forced_variant = v; }
 
@@ -576,12 +609,20 @@ char compress_variant(const CompressArgs &a) {
         forced = e && std::string(e) == "general" ? 'w' : 0;
     }
     if (forced == 'w') return 'w';
-    return split_stride_words(a) != 0 ? 's' : 'w';
+    if (split_stride_words(a) != 0 && forced != 'x') return 's';
+    return spec_applies(a, forced == 'x') ? 'x' : 'w';
 }
 
 hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;
-    if (compress_variant(a) == 's') return launch_compress_split(a, a.ht_global, st);
+    const char v = compress_variant(a);
+    if (v == 's') return launch_compress_split(a, a.ht_global, st);
+    // long fresh streams: K1x rounds, which call the general kernel to resolve emitting positions
+    if (v == 'x') return launch_compress_spec(a, (uint8_t *)a.ht_global, st);
+    return launch_general(a, st);
+}
+
+hipError_t launch_general(const CompressArgs &a, hipStream_t st) {
     const bool htl = a.hs <= kHtLdsMax;
     const bool pl = a.max_len > 0 && (int64_t)a.max_len <= kPLdsMax && !a.write_idx;  // multi-Write: the global view
     const bool ring = a.ring != nullptr;

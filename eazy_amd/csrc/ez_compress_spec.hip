@@ -1,0 +1,416 @@
+// ez_compress_spec.hip — K1x: data-parallel rounds for long fresh streams.
+//
+// The general kernel runs one wave per stream, so a batch of few long Writes (C4: 64 x 4 MiB
+// gradient buckets) keeps 64 of 1,024 SIMDs busy with a serial chain.  But between two emitting
+// positions Writer.Write (writer.go:206-337) is easy to predict: with the pending literal starting
+// at `from` (done = from, w.pos = from), every position x >= from is visited until one is
+// accepted, so the table at x is the table at `from` updated with every position of [from, x):
+// for each hash, the nearest earlier position of [from, x) with that hash, else the entry at
+// `from`.  Whether x is accepted then depends on x, that candidate and `from` only, so all
+// positions of a stream are judged at once and the first accepted one is kept.  A round:
+//   kx_reset  a stream without an accepted position last round is finished: one literal from
+//             `from` to its end (writer.go:324-329); the others are listed as active;
+//   kx_judge  (a thread per position of the active streams, from `from` on): candidate and test
+//             as writer.go:219-301 (writeRunlen :441-489, writeZeros :407-424) would have them;
+//             the first accepted position of a stream is kept (atomicMin);
+//   kx_merge  the table at that position, from the table at `from`, the scanned tables (below)
+//             and the positions of its chunk;
+//   general   (spec_mode 1) resumes each stream at that position with that table, takes the one
+//             action Go takes there (copy, cut or zero run) and stores its state back: the next
+//             round starts where that action ended.
+// Before the rounds: kx_init writes the headers; kx_pred hashes every position and finds the
+// nearest earlier same-hash position within its 16 Ki-position chunk, and each chunk's last
+// positions per hash; kx_scan turns those into each chunk's incoming table (the latest earlier
+// chunk's entry).  After the rounds the general kernel (spec_mode 2) takes the streams still
+// active from where they stand, and kx_copy writes every literal's bytes (the rounds and the
+// spec_mode 1 calls only write the tags and record the literals: a literal can be megabytes).
+// Exactness: x is judged against the table Go has there as long as no position of [from, x)
+// was accepted, and the first accepted one is found exactly; a position flagged wrongly would
+// only cost time (the general kernel judges it again and goes on), a missed one would not, so
+// the test below restates the general kernel's lane evaluation term for term.
+#include "ez_format.h"
+#include "ez_internal.h"
+#include "ez_wave.h"
+#include "ez_bytes.h"
+
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <vector>
+
+namespace ez {
+namespace {
+
+constexpr int64_t kChunk = 16384;     // positions per kx_pred chunk (chunk-local distances fit u16)
+constexpr uint32_t kNone = 0xffffffffu;
+constexpr int64_t kPiece = 256;       // kx_judge: positions per block step
+constexpr int64_t kCopyPiece = 65536; // kx_copy: bytes per block step
+constexpr int kRounds = 8;            // rounds before the general kernel takes the rest (EZ_K1X_ROUNDS)
+
+struct KxBufs {
+    uint64_t kmax;     // chunks per stream
+    uint16_t *pred;    // per input byte: distance to the nearest earlier same-hash position of its chunk (0: none)
+    uint32_t *tabs;    // per chunk and hash: the incoming entry (after kx_scan)
+    uint32_t *first;   // per stream: the round's first accepted position (kNone: none)
+    uint32_t *act;     // active streams of the round
+    uint32_t *nact;    // [0] active count, [1] literal records
+    uint64_t lit_cap;  // literal records reserved
+};
+
+__device__ __forceinline__ uint32_t hash4(const uint8_t *q, uint32_t hsh) {
+    const uint32_t v = (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) | ((uint32_t)q[3] << 24);
+    return (v * kHashMul) >> hsh;
+}
+
+__device__ __forceinline__ uint32_t hshift(int64_t hs) { return 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(hs - 1))); }
+
+__device__ __forceinline__ int64_t slen(const CompressArgs &A, uint64_t s) { return (int64_t)(A.in_off[s + 1] - A.in_off[s]); }
+
+// stream s's header (writer.go:495-517), its state at position 0, its table zeroed
+__global__ __launch_bounds__(64) void kx_init(CompressArgs A, KxBufs B) {
+    const uint64_t s = blockIdx.x;
+    const int lane = (int)threadIdx.x;
+    if (s == 0 && lane == 0) B.nact[1] = 0;
+    for (int64_t h = lane; h < A.hs; h += 64) A.spec_tab[s * (uint64_t)A.hs + h] = 0;
+    if (lane != 0) return;
+    Hdr h;
+    if (A.append_magic) { h.put(0x80); h.put(0x02); h.put('e'); h.put('a'); h.put('z'); h.put('y'); }
+    if (A.ver != 0) { h.put(0x80); h.put(0x08); h.put((uint32_t)A.ver); }
+    h.put(0x80); h.put(0x10); h.put((uint32_t)__builtin_ctzll((uint64_t)A.bs));
+    const int64_t cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    B.first[s] = 0;  // active in round 1
+    // the launcher sized the scratch from max_len: longer streams are refused (as K1s does);
+    // a header that does not fit is not written (put_hdr)
+    const int err = (uint64_t)slen(A, s) > A.max_len ? EZ_EINVAL : (h.n > cap ? EZ_ENOSPC : EZ_OK);
+    if (err) {
+        A.spec[s] = SpecState{0u, 0u, 0u, 1u};
+        A.out_size[s] = 0;
+        if (A.status) A.status[s] = err;
+        return;
+    }
+    uint8_t *o = A.out + A.out_off[s];
+    for (int k = 0; k < h.n; k++) o[k] = h.byte(k);
+    A.spec[s] = SpecState{0u, 0u, (uint32_t)h.n, 0u};
+}
+
+// chunk (s, k): block s * kmax + k, one wave
+__global__ __launch_bounds__(64) void kx_pred(CompressArgs A, KxBufs B) {
+    extern __shared__ uint32_t T[];
+    const uint64_t s = blockIdx.x / B.kmax, k = blockIdx.x % B.kmax;
+    const int lane = (int)threadIdx.x;
+    const int64_t n = slen(A, s);
+    const int64_t lo = (int64_t)k * kChunk;
+    if (lo + 4 > n || (uint64_t)n > A.max_len) return;
+    const uint8_t *p = A.in + A.in_off[s];
+    uint16_t *pr = B.pred + (A.in_off[s] - A.in_off[0]);  // offsets are absolute (views of a larger batch)
+    const uint32_t hsh = hshift(A.hs);
+    for (int64_t h = lane; h < A.hs; h += 64) T[h] = kNone;
+    __syncthreads();
+    const int64_t hi = lo + kChunk < n - 3 ? lo + kChunk : n - 3;  // hashed positions: x + 4 <= n
+    for (int64_t b = lo; b < hi; b += 64) {
+        const int64_t x = b + lane;
+        if (x < hi) {
+            const uint32_t h = hash4(p + x, hsh);
+            // lane-ordered exchange: the previous value is the nearest earlier position of the
+            // chunk with this hash (an earlier lane of this step, or an earlier step)
+            const uint32_t prev = atomicExch(&T[h], (uint32_t)x);
+            pr[x] = prev == kNone ? (uint16_t)0 : (uint16_t)(x - (int64_t)prev);
+        }
+    }
+    __syncthreads();
+    uint32_t *tab = B.tabs + (uint64_t)blockIdx.x * (uint64_t)A.hs;
+    for (int64_t h = lane; h < A.hs; h += 64) tab[h] = T[h];
+}
+
+// thread (s, h): incoming entry of every chunk of stream s, in place (0: none before the chunk)
+__global__ __launch_bounds__(256) void kx_scan(CompressArgs A, KxBufs B) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t s = t / (uint64_t)A.hs, h = t % (uint64_t)A.hs;
+    if (s >= A.count) return;
+    const int64_t n = slen(A, s);
+    const uint64_t kn = n > 3 ? (uint64_t)((n - 3 + kChunk - 1) / kChunk) : 0;
+    uint32_t run = 0;
+    for (uint64_t k = 0; k < kn && k < B.kmax; k++) {
+        uint32_t *e = B.tabs + (s * B.kmax + k) * (uint64_t)A.hs + h;
+        const uint32_t v = *e;
+        *e = run;
+        if (v != kNone) run = v;
+    }
+}
+
+// the trailing literal of a stream with nothing more to accept: its tag now, its bytes in kx_copy
+__device__ void kx_tail(const CompressArgs &A, const KxBufs &B, uint64_t s) {
+    const SpecState sp = A.spec[s];
+    const int64_t n = slen(A, s), done = sp.done;
+    int64_t op = sp.op;
+    const int64_t cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    int err = EZ_OK;
+    if (done < n) {
+        Hdr h;
+        if (!hdr_tag(h, kLiteral, n - done)) err = EZ_EINVAL;
+        else if (op + h.n > cap) err = EZ_ENOSPC;
+        else {
+            uint8_t *o = A.out + A.out_off[s] + op;
+            for (int k = 0; k < h.n; k++) o[k] = h.byte(k);
+            op += h.n;
+            if (op + (n - done) > cap) err = EZ_ENOSPC;
+            else {
+                A.spec_lit[atomicAdd(&B.nact[1], 1u)] = SpecLit{A.in_off[s] + (uint64_t)done, A.out_off[s] + (uint64_t)op, (uint64_t)(n - done)};
+                op += n - done;
+            }
+        }
+    }
+    A.out_size[s] = (uint64_t)op;
+    if (A.status) A.status[s] = err;
+    A.spec[s].flags = 1u;
+}
+
+// one block: finish the streams whose last round accepted nothing, list the active ones
+__global__ __launch_bounds__(1024) void kx_reset(CompressArgs A, KxBufs B) {
+    __shared__ uint32_t cnt;
+    if (threadIdx.x == 0) cnt = 0;
+    __syncthreads();
+    for (uint64_t s = threadIdx.x; s < A.count; s += 1024) {
+        if (A.spec[s].flags != 0) continue;
+        if (B.first[s] == kNone) {
+            kx_tail(A, B, s);
+        } else {
+            B.first[s] = kNone;
+            B.act[atomicAdd(&cnt, 1u)] = (uint32_t)s;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) B.nact[0] = cnt;
+}
+
+// Would Go's parse, at x with the pending literal from `done` = w.pos (a fresh stream: start 0)
+// and candidate cand, take an action?  The general kernel's lane evaluation (ez_compress.hip,
+// "per-lane capped evaluation"), with 8-byte extensions: acceptance needs 6 bytes, and an
+// extension capped at 8 is accepted there before its exact length is known.
+__device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t *p, int64_t n, int64_t x, int64_t cand, int64_t done) {
+    const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
+    const V16 vx = ld_clamped(p + x - 8, lo, hi);  // stream bytes x-8 .. x+7
+    const int64_t bs = A.bs;
+    if (cand >= done && x > cand) {
+        // off >= 0 and i > done + off: writeRunlen with st = cand (writer.go:227-231, 441-473)
+        const V16 vc = ld_clamped(p + cand - 8, lo, hi);
+        if (cand + 8 < n && vc.hi == 0) return true;  // writeZeros: >= 8 zeros at st
+        const uint64_t df = vx.hi ^ vc.hi, db = vx.lo ^ vc.lo;
+        int64_t f = df ? (int64_t)(__builtin_ctzll(df) >> 3) : 8;
+        f = f < n - x ? f : n - x;
+        int64_t c = db ? (int64_t)(__builtin_clzll(db) >> 3) : 8;
+        const int64_t cl = cand < x - done ? cand : x - done;
+        c = c < cl ? c : cl;
+        return f + c >= kMinCopyChunk;  // a run or the cut branch: both emit
+    }
+    if (done - cand > bs) return false;  // far skip (writer.go:221-224)
+    // window match against the ring image at w.pos = done (writer.go:233-301): block[y & mask]
+    // holds stream byte done - bs + ((y - done) & mask), zero before the stream
+    V16 vc;
+    if (cand - 8 >= 0 && cand - 8 >= done - bs && cand + 8 <= done) {
+        vc = ld16v(p + cand - 8);
+    } else {
+        vc = V16{0, 0};
+        const int64_t mask = bs - 1;
+        for (int t = 0; t < 16; t++) {
+            const int64_t q = done - bs + ((cand - 8 + t - done) & mask);
+            const uint64_t b = q >= 0 ? p[q] : 0;
+            if (t < 8) vc.lo |= b << (8 * t);
+            else vc.hi |= b << (8 * (t - 8));
+        }
+    }
+    const uint64_t df = vx.hi ^ vc.hi, db = vx.lo ^ vc.lo;
+    int64_t f = df ? (int64_t)(__builtin_ctzll(df) >> 3) : 8;
+    f = f < n - x ? f : n - x;
+    int64_t c = db ? (int64_t)(__builtin_clzll(db) >> 3) : 8;
+    c = c < x - done ? c : x - done;
+    // the two trims (writer.go:280-291): the copy stays within bs of x and ends by w.pos
+    int64_t len = f + c;
+    const int64_t t1 = bs - (x - cand), t2 = done - cand + c;
+    len = len < t1 ? len : t1;
+    len = len < t2 ? len : t2;
+    return len >= kMinCopyChunk;
+}
+
+// blocks step over (piece j, active stream a), pieces of 256 positions from `from` on, so the
+// early pieces of every active stream are judged first and a stream's later pieces are skipped
+// once an accepted position before them is known
+__global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
+    const uint64_t nact = B.nact[0];
+    const uint64_t kp = (A.max_len + kPiece - 1) / kPiece + 1;
+    const uint32_t hsh = hshift(A.hs);
+    const int lane = (int)(threadIdx.x & 63);
+    for (uint64_t q = blockIdx.x; q < nact * kp; q += gridDim.x) {
+        const uint64_t j = q / nact, s = B.act[q % nact];
+        const SpecState sp = A.spec[s];
+        const int64_t n = slen(A, s), from = sp.from, done = sp.done;
+        const int64_t xb = (from & ~(kPiece - 1)) + (int64_t)j * kPiece;
+        if (xb + 4 > n || xb > (int64_t)__atomic_load_n(&B.first[s], __ATOMIC_RELAXED)) continue;
+        const int64_t x = xb + threadIdx.x;
+        bool acc = false;
+        if (x >= from && x + 4 <= n) {
+            const uint8_t *p = A.in + A.in_off[s];
+            const uint32_t h = hash4(p + x, hsh);
+            const uint16_t d = B.pred[A.in_off[s] - A.in_off[0] + x];
+            // nearest earlier same-hash position (chunk-local, else the chunk's incoming entry);
+            // before `from` the table at `from` holds the entry
+            const int64_t pc = d ? x - d : (int64_t)B.tabs[(s * B.kmax + (uint64_t)(x / kChunk)) * (uint64_t)A.hs + h];
+            const int64_t cand = pc >= from ? pc : (int64_t)A.spec_tab[s * (uint64_t)A.hs + h];
+            acc = kx_accepts(A, p, n, x, cand, done);
+        }
+        const uint64_t m = wballot(acc);
+        if (m && lane == ffs64(m)) atomicMin(&B.first[s], (uint32_t)x);
+    }
+}
+
+// the table at first[s]: the table at `from`, then every position of [from, first) in order,
+// last writer wins (not the largest: after a cut, writer.go:464-473, `from` can lie before
+// positions the table already holds, and Go visits them again)
+__global__ __launch_bounds__(256) void kx_merge(CompressArgs A, KxBufs B) {
+    extern __shared__ uint32_t T[];
+    uint32_t *U = T + A.hs;  // 1 + the last position of the current chunk's part, 0: none
+    const uint64_t s = blockIdx.x;
+    if (A.spec[s].flags != 0 || B.first[s] == kNone) return;
+    const int64_t from = A.spec[s].from, f = B.first[s];
+    uint32_t *tab = A.spec_tab + s * (uint64_t)A.hs;
+    const int64_t c = f / kChunk, cs = c * kChunk;
+    const uint32_t *inc = B.tabs + (s * B.kmax + (uint64_t)c) * (uint64_t)A.hs;
+    for (int64_t h = threadIdx.x; h < A.hs; h += 256) {
+        uint32_t v = tab[h];
+        // positions of [from, cs): the latest before the chunk, when it is not before `from`
+        if (from < cs && (int64_t)inc[h] >= from) v = inc[h];
+        T[h] = v;
+        U[h] = 0;
+    }
+    __syncthreads();
+    const uint8_t *p = A.in + A.in_off[s];
+    const uint32_t hsh = hshift(A.hs);
+    for (int64_t x = (cs > from ? cs : from) + threadIdx.x; x < f; x += 256) atomicMax(&U[hash4(p + x, hsh)], (uint32_t)x + 1u);
+    __syncthreads();
+    for (int64_t h = threadIdx.x; h < A.hs; h += 256) tab[h] = U[h] ? U[h] - 1u : T[h];
+}
+
+// every recorded literal's bytes, 64 KiB per block step
+__global__ __launch_bounds__(256) void kx_copy(CompressArgs A, KxBufs B) {
+    const uint64_t nl = B.nact[1] < B.lit_cap ? B.nact[1] : B.lit_cap;
+    const uint64_t kp = (A.max_len + kCopyPiece - 1) / kCopyPiece;
+    const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
+    for (uint64_t q = blockIdx.x; q < nl * kp; q += gridDim.x) {
+        const SpecLit L = A.spec_lit[q / kp];
+        const uint64_t b = (q % kp) * (uint64_t)kCopyPiece;
+        if (b >= L.len) continue;
+        const uint64_t e = b + kCopyPiece < L.len ? b + kCopyPiece : L.len;
+        const uint8_t *src = A.in + L.src;
+        uint8_t *dst = A.out + L.dst;
+        for (uint64_t k = b + 16 * threadIdx.x; k < e; k += 16 * 256) {
+            const V16 v = src + k + 16 <= hi ? ld16v(src + k) : ld_clamped(src + k, lo, hi);
+            if (k + 16 <= e) st16v(dst + k, v);
+            else put_small(dst + k, v, (uint32_t)(e - k));
+        }
+    }
+}
+
+int rounds() {
+    static const int r = [] {
+        const char *e = getenv("EZ_K1X_ROUNDS");
+        const int v = e ? atoi(e) : kRounds;
+        return v >= 0 && v <= 1024 ? v : kRounds;
+    }();
+    return r;
+}
+
+struct Layout {
+    uint64_t pred, tabs, first, spec, spec_tab, act, nact, lit, total, lit_cap;
+};
+
+Layout layout(const CompressArgs &a) {
+    const uint64_t kmax = (a.max_len + kChunk - 1) / kChunk;
+    auto up = [](uint64_t v) { return (v + 255) & ~255ull; };
+    Layout l;
+    l.lit_cap = a.count * (uint64_t)(2 * rounds() + 1);  // <= 2 per stream per round (general), 1 tail
+    l.pred = 0;
+    l.tabs = l.pred + up(a.count * a.max_len * 2);
+    l.first = l.tabs + up(a.count * kmax * (uint64_t)a.hs * 4);
+    l.spec = l.first + up(a.count * 4);
+    l.spec_tab = l.spec + up(a.count * sizeof(SpecState));
+    l.act = l.spec_tab + up(a.count * (uint64_t)a.hs * 4);
+    l.nact = l.act + up(a.count * 4);
+    l.lit = l.nact + 256;
+    l.total = l.lit + up(l.lit_cap * sizeof(SpecLit));
+    return l;
+}
+
+}  // namespace
+
+// Streams qualify when fresh, one Write each, at least 64 KiB long (below that the general
+// kernel's chain is short), their positions and outputs fit u32 and the table fits LDS; the
+// scratch (u16 per input byte, one table per chunk) stays bounded.
+bool spec_applies(const CompressArgs &a, bool any_len) {
+    static const bool off = getenv("EZ_K1X") && atoi(getenv("EZ_K1X")) == 0;  // A/B: the general kernel alone
+    if (off || a.max_len == 0 || a.ring || a.write_idx || a.start != 0 || !a.header || a.hs > 4096 || (a.max_len < (64u << 10) && !any_len) ||
+        a.max_len >= (1ull << 31) || a.count == 0)
+        return false;
+    const uint64_t chunks = a.count * ((a.max_len + kChunk - 1) / kChunk);
+    // kx_pred relies on lane-ordered LDS exchanges, as K1s-T32 (checked on the device once)
+    return chunks <= (1u << 20) && a.count * a.max_len <= (64ull << 30) && lds_exchange_in_lane_order();
+}
+
+uint64_t spec_scratch_bytes(const CompressArgs &a) { return layout(a).total; }
+
+hipError_t launch_compress_spec(const CompressArgs &a0, uint8_t *scratch, hipStream_t st) {
+    const Layout l = layout(a0);
+    KxBufs B;
+    B.kmax = (a0.max_len + kChunk - 1) / kChunk;
+    B.pred = (uint16_t *)(scratch + l.pred);
+    B.tabs = (uint32_t *)(scratch + l.tabs);
+    B.first = (uint32_t *)(scratch + l.first);
+    B.act = (uint32_t *)(scratch + l.act);
+    B.nact = (uint32_t *)(scratch + l.nact);
+    B.lit_cap = l.lit_cap;
+    CompressArgs a = a0;
+    a.spec = (SpecState *)(scratch + l.spec);
+    a.spec_first = B.first;
+    a.spec_tab = (uint32_t *)(scratch + l.spec_tab);
+    a.spec_lit = (SpecLit *)(scratch + l.lit);
+    a.spec_nlit = &B.nact[1];
+    hipError_t e;
+    auto check = [&]() { return (e = hipGetLastError()) == hipSuccess; };
+    const unsigned count = (unsigned)a.count;
+    const unsigned chunks = (unsigned)(a.count * B.kmax);
+    const size_t tlds = (size_t)a.hs * 4;
+    hipLaunchKernelGGL(kx_init, dim3(count), dim3(64), 0, st, a, B);
+    if (!check()) return e;
+    hipLaunchKernelGGL(kx_pred, dim3(chunks), dim3(64), tlds, st, a, B);
+    if (!check()) return e;
+    hipLaunchKernelGGL(kx_scan, dim3((unsigned)((a.count * (uint64_t)a.hs + 255) / 256)), dim3(256), 0, st, a, B);
+    if (!check()) return e;
+    const unsigned jgrid = 2048;  // 8 blocks of 4 waves per CU
+    for (int r = 0; r < rounds(); r++) {
+        hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B);
+        if (!check()) return e;
+        hipLaunchKernelGGL(kx_judge, dim3(jgrid), dim3(256), 0, st, a, B);
+        if (!check()) return e;
+        hipLaunchKernelGGL(kx_merge, dim3(count), dim3(256), 2 * tlds, st, a, B);
+        if (!check()) return e;
+        a.spec_mode = 1;
+        if ((e = launch_general(a, st)) != hipSuccess) return e;
+    }
+    // the streams still active: the general kernel from where they stand; then every literal's bytes
+    hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B);
+    if (!check()) return e;
+    a.spec_mode = 2;
+    if ((e = launch_general(a, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(kx_copy, dim3(jgrid), dim3(256), 0, st, a, B);
+    if (!check()) return e;
+    if (getenv("EZ_K1X_DEBUG")) {  // diagnostics: streams left to the general kernel's serial continuation
+        std::vector<SpecState> h(a.count);
+        uint32_t nl[2];
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpy(h.data(), a.spec, a.count * sizeof(SpecState), hipMemcpyDeviceToHost);
+        (void)hipMemcpy(nl, B.nact, 8, hipMemcpyDeviceToHost);
+        fprintf(stderr, "K1x: %d rounds, %u literal records; active after the rounds: %u\n", rounds(), nl[1], nl[0]);
+    }
+    return hipSuccess;
+}
+
+}  // namespace ez

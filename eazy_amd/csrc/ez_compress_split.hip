@@ -469,7 +469,11 @@ typedef const __attribute__((address_space(1))) u32x4 *gu128p;
 struct LeanIn {
     __device__ __forceinline__ uint32_t dw(const uint8_t *w) const { return *(gu32p)w; }
     __device__ __forceinline__ uint4 dw4(const uint8_t *w) const {
+#if (EZ_EXP & 16)
+        const u32x4 v = __builtin_nontemporal_load((gu128p)w);
+#else
         const u32x4 v = *(gu128p)w;
+#endif
         return make_uint4(v.x, v.y, v.z, v.w);
     }
 };

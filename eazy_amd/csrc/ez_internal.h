@@ -7,6 +7,16 @@
 
 namespace ez {
 
+// K1x per-stream state (ez_compress_spec.hip): speculation restarts at `from`, the pending literal
+// starts at `done`, the stream's output so far is `op` bytes; flags: 0 active, 1 finished
+struct SpecState {
+    uint32_t from, done, op, flags;
+};
+// a literal whose bytes K1x copies at the end (kx_copy): len bytes from in[src] to out[dst]
+struct SpecLit {
+    uint64_t src, dst, len;
+};
+
 // One K1 launch: `count` independent streams (batch) or one stream of a
 // writer handle (ring != nullptr, ht_global persistent).
 struct CompressArgs {
@@ -32,7 +42,20 @@ struct CompressArgs {
     const uint64_t *write_idx;
     const uint64_t *write_end;
     uint64_t max_writes;      // the most Writes of one stream (records reserved for their ends)
+    // K1x rounds (ez_compress_spec.hip): the general kernel resumes a stream from K1x's state
+    //   spec_mode 1: at spec_first[s] (streams with ~0u there are skipped), with the table
+    //                spec_tab[s]; stops after the first accepted copy and stores its state back;
+    //                its literals' bytes are left to kx_copy (a record in spec_lit each)
+    //   spec_mode 2: at spec[s].from, to the end of the stream
+    // streams whose spec[s].flags != 0 are finished and skipped
+    int spec_mode;
+    SpecState *spec;
+    const uint32_t *spec_first;
+    uint32_t *spec_tab;
+    SpecLit *spec_lit;
+    uint32_t *spec_nlit;
 };
+
 
 // One K2 launch.  Batch: count complete streams from fresh Readers.
 // Handle: count == 1 with the streaming state in `st`.
@@ -83,6 +106,12 @@ hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipSt
 // the K1 kernel a batch launch takes: 's' K1s (parse + token writer), 'w' general wave per stream
 char compress_variant(const CompressArgs &a);
 void select_compress_variant(int v);  // 0 = automatic, else a variant letter (tests, A/B)
+// K1x: the data-parallel first pass for long fresh single-Write streams (ez_compress_spec.hip)
+bool spec_applies(const CompressArgs &a, bool any_len = false);  // any_len: also below 64 KiB (forced)
+uint64_t spec_scratch_bytes(const CompressArgs &a);
+hipError_t launch_compress_spec(const CompressArgs &a, uint8_t *scratch, hipStream_t s);
+// the general kernel for one launch (ez_compress.hip); K1x calls it in its resume modes
+hipError_t launch_general(const CompressArgs &a, hipStream_t s);
 // u32 words of global hash-table scratch a batch launch needs (hs too big for LDS)
 uint64_t compress_scratch_words(const CompressArgs &a);
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t s);

@@ -174,12 +174,15 @@ int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *works
 /* Introspection (no reference counterpart): the K1 kernel a batch of `count`
  * fresh streams of <= max_len bytes would run on the current device, as a
  * character: 's' K1s (parse + token writer; fresh streams with 2n <= block and
- * at most 4096 table entries), 'w' general wave per stream (everything else);
+ * at most 4096 table entries), 'x' K1x (data-parallel rounds over the emitting
+ * positions, then the general kernel; other fresh single-Write batches of streams
+ * up to 2 GiB, at least one of 64 KiB or more, at most 4096 table entries),
+ * 'w' general wave per stream (everything else);
  * EZ_EDEVICE (negated) without a device. */
 int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t count);
 /* Testing / A-B measurement (no reference counterpart): force the K1 kernel of
  * later batch calls in this process ('s' K1s, 'S' K1s with the u32
- * exchange table, 'w' general; 0 = automatic choice).  A forced kernel that cannot take a batch falls
+ * exchange table, 'w' general alone, 'x' K1x at any stream length; 0 = automatic choice).  A forced kernel that cannot take a batch falls
  * back to the automatic choice.  Not thread-safe against concurrent calls. */
 int ez_select_compress_kernel(int kind);
 /* Testing / A-B measurement: the first K2 kernel of later batch decodes with a

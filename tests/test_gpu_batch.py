@@ -13,11 +13,12 @@ pytestmark = pytest.mark.gpu
 MiB = 1 << 20
 
 
-@pytest.fixture(params=["", "S", "w"], ids=["auto", "split32", "general"], autouse=True)
+@pytest.fixture(params=["", "S", "w", "x"], ids=["auto", "split32", "general", "k1x"], autouse=True)
 def k1_kind(request):
     """Every batch test runs on the automatic K1 choice (K1s: the lean parse on the u16
-    table at these shapes), on K1s with the u32 exchange table forced, and on the
-    general wave-per-stream kernel forced."""
+    table at these shapes), on K1s with the u32 exchange table forced, on the
+    general wave-per-stream kernel forced, and on K1x's rounds forced (where a batch
+    qualifies: fresh single Writes, table <= 4096 entries)."""
     import eazy_amd as ez
 
     ez.select_compress_kernel(request.param)
@@ -163,7 +164,9 @@ def test_split_kernel_selected(cuda, k1_kind):
     want = {"": "s", "S": "s"}.get(k1_kind, k1_kind)
     assert ez.compress_kernel(MiB, 1024, 4096, 65536) == want
     assert ez.compress_kernel(MiB, 1 << 13, 4096, 65536) == "w"  # tables over 4096 entries: the general kernel
-    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) == "w"  # 2n > block: only the general kernel
+    # 2n > block: K1x's rounds, then the general kernel (forced 'w': the general kernel alone)
+    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) == ("w" if k1_kind == "w" else "x")
+    assert ez.compress_kernel(MiB, 1 << 13, 1 << 20, 4) == "w"
 
 
 def _multi_write_check(cuda, streams, block=MiB, htable=1024):
@@ -304,3 +307,46 @@ def test_batch_edge_streams(cuda, k1_kind):
     _check(cuda, [b"abcabcabcab"])
     _check(cuda, [d[:4096]])
     _check(cuda, [b"", d[:6000], b""])
+
+
+def _planted(rng, n, events, block, zeros=False):
+    """n random bytes with `events` copies planted: 6..40 bytes repeated from up to
+    `block` + 64 bytes back (window matches, far skips, cuts), runs, and zero runs."""
+    b = bytearray(rng.integers(0, 256, n, dtype=np.uint8).tobytes())
+    for p in np.sort(rng.integers(64, n - 64, events)):
+        p = int(p)
+        kind = int(rng.integers(0, 4 if zeros else 3))
+        L = int(rng.integers(5, 40))
+        if kind == 0:  # an earlier stretch
+            d = int(rng.integers(1, min(p, block + 64)))
+            for t in range(min(L, n - p)):
+                b[p + t] = b[p - d + t]
+        elif kind == 1:  # a short-period run
+            per = int(rng.integers(1, 9))
+            for t in range(per, min(L, n - p)):
+                b[p + t] = b[p + t - per]
+        elif kind == 2:  # the stream's first bytes again
+            b[p : p + L] = b[:L]
+        else:
+            b[p : p + L] = bytes(L)
+    return bytes(b)
+
+
+def test_k1x_rounds(cuda, k1_kind):
+    """K1x (ez_compress_spec.hip): fresh long streams whose emitting positions are judged all
+    at once, one round per accepted position, the general kernel resolving each and taking
+    the rest after 8 rounds.  Planted matches at every distance up to past the window, runs,
+    zero runs, the stream's first bytes, fewer and more events than rounds, empty and tiny
+    streams beside long ones; block 1 MiB / 4 KiB / 1 KiB, tables 16 .. 4096 entries."""
+    if k1_kind not in ("", "x"):
+        pytest.skip("K1x's own shapes (the automatic choice and K1x forced)")
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(41)
+    f = synth.f32(43, 1 << 16).view(np.uint8).tobytes()
+    bufs = [_planted(rng, 70000, e, MiB, zeros=e % 2 == 1) for e in (0, 1, 2, 5, 7, 8, 9, 20)]
+    bufs += [f[: 1 << 18], (f[:100000] + bytes(300) + f[:70000]), b"", b"ab", b"abcde"]
+    _check(cuda, bufs)
+    small = [_planted(rng, 80000, e, 4096, zeros=True) for e in (3, 12, 40)]
+    for block, htable in ((4096, 16), (4096, 4096), (1024, 256)):
+        _check(cuda, small, block, htable)
