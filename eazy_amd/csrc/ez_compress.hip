@@ -43,6 +43,7 @@ constexpr int kMaskBytes = kBuckets * 8;
 constexpr int kHashBytes = kWave * 4;
 constexpr int64_t kPLdsMax = 16 * 1024;  // stage streams up to this size in LDS
 constexpr int64_t kHtLdsMax = 4096;      // hash tables up to this many entries in LDS
+constexpr uint32_t kWinBytes = 32768;    // LDS window of a long stream (EZ_K1W_WIN, 0: none)
 
 enum Kind : int { kReject = 0, kWin = 1, kRun = 2, kCut = 3, kZero = 4 };
 
@@ -57,13 +58,41 @@ struct InView {
     uint64_t glast;        // last valid word index of gw
     const uint32_t *lw;    // LDS words (PL)
     uint32_t lr;           // byte misalignment inside lw (PL)
+    // !PL, long streams: an LDS window of the stream around the parse position, so that the
+    // reads near i (the next window's bytes, zero runs, literals) are LDS reads, not one HBM
+    // round trip each: ww[k] = gw-relative bytes wa0 + 4k .. (wnb bytes held)
+    const uint32_t *ww = nullptr;
+    int64_t wa0 = 0;
+    uint64_t wnb = 0;
 
+    // window offset of stream byte x, when [x, x+k) is held
+    __device__ __forceinline__ bool inw(int64_t x, int64_t k, uint64_t &a) const {
+        const int64_t sa = (int64_t)gr + x - wa0;
+        a = (uint64_t)sa;
+        return !PL && ww && sa >= 0 && sa + k <= (int64_t)wnb;
+    }
+    // 16 window bytes at window offset a (aligned words + byte shifts)
+    __device__ __forceinline__ V16 wv16(uint64_t a) const {
+        const uint32_t *w = ww + (a >> 2);
+        const uint32_t r = (uint32_t)(a & 3);
+        const uint32_t d0 = w[0], d1 = w[1], d2 = w[2], d3 = w[3], d4 = w[4];
+        const uint32_t e0 = __builtin_amdgcn_alignbyte(d1, d0, r), e1 = __builtin_amdgcn_alignbyte(d2, d1, r);
+        const uint32_t e2 = __builtin_amdgcn_alignbyte(d3, d2, r), e3 = __builtin_amdgcn_alignbyte(d4, d3, r);
+        return V16{(uint64_t)e0 | ((uint64_t)e1 << 32), (uint64_t)e2 | ((uint64_t)e3 << 32)};
+    }
     __device__ __forceinline__ uint32_t b(int64_t x) const {
         if (PL) return ((const uint8_t *)lw)[lr + (uint64_t)x];
+        uint64_t a;
+#if (EZ_EXP & 32)
+        if (inw(x, 1, a) && ((const uint8_t *)ww)[a] != g[x]) printf("b mismatch x %lld a %llu wa0 %lld wnb %llu\n", (long long)x, (unsigned long long)a, (long long)wa0, (unsigned long long)wnb);
+#endif
+        if (inw(x, 1, a)) return ((const uint8_t *)ww)[a];
         return g[x];
     }
     __device__ __forceinline__ uint32_t u32(int64_t x) const {
         if (PL) return words_u32(lw, lr + (uint64_t)x);
+        uint64_t wa;
+        if (inw(x, 4, wa)) return words_u32(ww, wa);
         const uint64_t a = gr + (uint64_t)x;
         const uint64_t k = a >> 2;
         const uint32_t w0 = gw[k];
@@ -92,11 +121,12 @@ __device__ __forceinline__ void put_bytes(OutBuf &o, const V &P, int64_t src, in
     if (o.op + L > o.cap) { o.err = EZ_ENOSPC; return; }
     uint8_t *d = o.p + o.op;
     if (!V::kLds && L >= 64) {
-        // global input: 16 bytes per lane, 1 KiB per wave step (a fresh stream's
-        // trailing literal is the whole Write when nothing matches, C4)
+        // global input (or the LDS window): 16 bytes per lane, 1 KiB per wave step (a fresh
+        // stream's trailing literal is the whole Write when nothing matches, C4)
         const uint8_t *q = P.g + src;
         for (int64_t k = 16 * lane; k < L; k += 16 * kWave) {
-            const V16 v = q + k + 16 <= P.hi ? ld16v(q + k) : ld_clamped(q + k, P.lo, P.hi);
+            uint64_t wa;
+            const V16 v = P.inw(src + k, 16, wa) ? P.wv16(wa) : q + k + 16 <= P.hi ? ld16v(q + k) : ld_clamped(q + k, P.lo, P.hi);
             if (k + 16 <= L) st16v(d + k, v);
             else put_small(d + k, v, (uint32_t)(L - k));
         }
@@ -149,8 +179,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
 
     // ---- LDS carve (all offsets 16-aligned)
     const uint64_t ht_bytes = HTL ? (uint64_t)hs * 4 : 0;
-    uint64_t *bmask = (uint64_t *)(smem + ht_bytes);
-    uint32_t *H = (uint32_t *)(smem + ht_bytes + kMaskBytes);
+    // (smem + ht_bytes: kMaskBytes + kHashBytes of scratch, unused since the ballot hash match)
     uint32_t *lw = (uint32_t *)(smem + ht_bytes + kMaskBytes + kHashBytes);
     // FP: beside every table entry, the 16 stream bytes around the position it holds
     // (x-8 .. x+7), so that a candidate is judged without loading its bytes
@@ -176,9 +205,47 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         for (uint64_t k = lane; k < nw; k += kWave) lw[k] = P.gw[k];
         if (lane < 4) lw[nw + lane] = 0;
     }
-    // ---- hash table and bucket masks
     // K1x resume: the table K1x prepared (spec_mode 1: at its first emitting position; 2: at from)
     const int smode = RING ? 0 : A.spec_mode;
+    // long streams: the LDS window (A.win_bytes, after the fingerprints), slid along with the
+    // parse; not for spec_mode 1, which takes one action per call
+    uint4 *win = (uint4 *)(smem + ht_bytes + kMaskBytes + kHashBytes + (FP ? (uint64_t)hs * 16 : 0));
+    const bool wl = !PL && !RING && !mw && A.win_bytes != 0 && smode != 1 && A.in_off[A.count] >= 16;
+    bool wend = false;  // the window reaches the stream's (or the batch's) end: no later refill
+    // window from stream position base (16-byte aligned addresses, inside the batch)
+    auto refill = [&](int64_t base) {
+        const uint64_t ga = (uint64_t)(uintptr_t)P.gw;
+        int64_t a0 = (int64_t)(((ga + P.gr + (uint64_t)base) & ~15ull) - ga);
+        if (ga + (uint64_t)a0 < (uint64_t)(uintptr_t)P.lo) a0 += 16;
+        int64_t n16 = (int64_t)(A.win_bytes / 16);
+        const int64_t max16 = (int64_t)(((uint64_t)(uintptr_t)P.hi - (ga + (uint64_t)a0)) / 16);
+        const int64_t need16 = ((int64_t)P.gr + n + 16 - a0 + 15) / 16;
+        if (n16 >= need16 || n16 >= max16) {
+            wend = true;
+            n16 = need16 < max16 ? need16 : max16;
+        }
+        __syncthreads();  // the old window's readers are done
+        const uint4 *src = (const uint4 *)(ga + (uint64_t)a0);
+#pragma unroll 8
+        for (int64_t k = lane; k < n16; k += kWave) win[k] = src[k];
+        if (lane < 2) win[n16 + lane] = make_uint4(0, 0, 0, 0);
+        __syncthreads();
+        P.ww = (const uint32_t *)win;
+        P.wa0 = a0;
+        P.wnb = (uint64_t)n16 * 16;
+#if (EZ_EXP & 32)
+        for (int64_t k = lane; k < n16 * 16; k += kWave)
+            if (((const uint8_t *)win)[k] != ((const uint8_t *)src)[k]) printf("refill mismatch k %lld base %lld\n", (long long)k, (long long)base);
+        for (int64_t x = base + lane; x < base + 64; x += kWave) {
+            uint64_t wa;
+            if (P.inw(x, 16, wa)) {
+                const V16 v = P.wv16(wa), gv = ld16v(P.g + x);
+                if (v.lo != gv.lo || v.hi != gv.hi) printf("wv16 mismatch x %lld\n", (long long)x);
+            }
+        }
+#endif
+    };
+    // ---- hash table and bucket masks
     if (HTL) {
         if (RING) for (int64_t k = lane; k < hs; k += kWave) ht[k] = A.ht_global[k];
         else if (smode) for (int64_t k = lane; k < hs; k += kWave) ht[k] = A.spec_tab[s * (uint64_t)hs + k];
@@ -186,7 +253,6 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     } else if (!RING) {
         for (int64_t k = lane; k < hs; k += kWave) ht[k] = 0;
     }
-    for (int k = lane; k < kBuckets; k += kWave) bmask[k] = 0;
     __syncthreads();
 
     OutBuf o;
@@ -218,6 +284,8 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     // bytes or to the zero history before a fresh stream (false: take the byte loop)
     const uint8_t *in_lo = A.in, *in_hi = A.in + A.in_off[A.count];
     auto s8 = [&](int64_t y) -> uint64_t {
+        uint64_t wa;
+        if (P.inw(y, 8, wa)) return P.wv16(wa).lo;
         const uint8_t *q = P.g + y;
         if (q >= in_lo && q + 8 <= in_hi) return *(const uint64_t __attribute__((aligned(1))) *)q;
         return (in_hi - in_lo >= 16) ? ld_clamped(q, in_lo, in_hi).lo : 0ull;
@@ -253,20 +321,43 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         // the window after this one if nothing is accepted (loaded while this one is judged)
         const bool pf = !PL && in_hi - in_lo >= 16;
         auto around = [&](int64_t y) -> V16 {
+            uint64_t wa;
+            if (P.inw(y - 8, 16, wa)) return P.wv16(wa);
             const uint8_t *q = P.g + y - 8;
             return q >= in_lo && q + 16 <= in_hi ? ld16v(q) : ld_clamped(q, in_lo, in_hi);
         };
         V16 nxt_w{0, 0};
         int64_t nxt_i = -1;
-        const bool usefp = FP && pf && start == 0 && !smode;
-        if (usefp) {  // the zero entries hold stream position 0
-            const V16 z = around(0);
-            for (int64_t k = lane; k < hs; k += kWave) fp[k] = z;
+        const bool usefp = FP && pf && start == 0 && smode != 1;
+        if (usefp) {
+            if (smode == 2) {  // K1x's table: the bytes around each entry's position
+#pragma unroll 4
+                for (int64_t k = lane; k < hs; k += kWave) fp[k] = around((int64_t)ht[k]);
+            } else {  // the zero entries hold stream position 0
+                const V16 z = around(0);
+                for (int64_t k = lane; k < hs; k += kWave) fp[k] = z;
+            }
             __syncthreads();
         }
 
+#if (EZ_EXP & 64)  // phase timers (debug): cycles per phase, events, iterations; stream 0 prints them
+        uint64_t tph[8] = {0, 0, 0, 0, 0, 0, 0, 0}, tlast = clock64(), nit = 0, nev = 0;
+#define EZ_T(k) do { const uint64_t t_ = clock64(); tph[k] += t_ - tlast; tlast = t_; } while (0)
+#else
+#define EZ_T(k) do {} while (0)
+#endif
         while (i + 4 <= n && !o.err) {
             if (++guard > guard_max) { o.err = EZ_ESTUCK; break; }
+#if (EZ_EXP & 64)
+            nit++;
+#endif
+            if (wl) {  // the window holds [i - 64, i + 192) unless it already reaches the end
+                const int64_t wlo = P.wa0 - (int64_t)P.gr, whi = wlo + (int64_t)P.wnb;
+                if (P.ww == nullptr || (i + 192 > whi && !wend) || (i - 64 < wlo && wlo > 0)) {
+                    wend = false;
+                    refill(i > 512 ? i - 512 : 0);
+                }
+            }
             const int64_t wpos = start + done;
             const int64_t rem = n - 3 - i;
             const int nvalid = rem < kWave ? (int)rem : kWave;
@@ -279,30 +370,24 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 nxt_i = i + nvalid;
             }
 
+            EZ_T(0);
             // -- hash + intra-window predecessor / successor with the same hash
             uint32_t h = 0xffffffffu;
             if (valid) h = ((pf ? (uint32_t)cur.hi : P.u32(x)) * kHashMul) >> hsh;
-            const int bk = (int)(h & (kBuckets - 1));
-            if (valid) {
-                atomicOr((unsigned long long *)&bmask[bk], 1ull << lane);
-                H[lane] = h;
+            // the lanes with this lane's hash: one ballot per hash bit (no LDS, no atomics: a zero
+            // run puts most lanes of a window on one hash, C4s)
+            uint64_t same = wballot(valid);
+            for (unsigned bit = 0; bit < 32u - hsh; bit++) {
+                const bool v = (h >> bit) & 1u;
+                const uint64_t bb = wballot(v);
+                same &= v ? bb : ~bb;
             }
-            __syncthreads();
             int prev = -1, next = kWave;
             if (valid) {
-                const uint64_t m = bmask[bk];
-                uint64_t below = m & ((1ull << lane) - 1);
-                while (below) {
-                    const int k = 63 - __builtin_clzll(below);
-                    if (H[k] == h) { prev = k; break; }
-                    below &= ~(1ull << k);
-                }
-                uint64_t above = lane == 63 ? 0ull : (m & (~0ull << (lane + 1)));
-                while (above) {
-                    const int k = __builtin_ctzll(above);
-                    if (H[k] == h) { next = k; break; }
-                    above &= above - 1;
-                }
+                const uint64_t below = same & ((1ull << lane) - 1);
+                const uint64_t above = lane == 63 ? 0ull : (same & (~0ull << (lane + 1)));
+                if (below) prev = 63 - __builtin_clzll(below);
+                if (above) next = __builtin_ctzll(above);
             }
             int64_t cand = 0;
             if (valid) cand = prev >= 0 ? (int64_t)(uint32_t)(start + i + prev) : (int64_t)ht[h];
@@ -314,6 +399,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 if (valid) cv = prev >= 0 ? pv : fp[h];
             }
 
+            EZ_T(1);
             // -- per-lane capped evaluation
             int kind = kReject;
             bool exact = true;
@@ -394,6 +480,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 }
             }
 
+            EZ_T(2);
             // -- first lane that accepts (exact resolution, wave-wide)
             uint64_t cm = wballot(valid && kind != kReject);
             const uint64_t exm = wballot(exact);
@@ -451,15 +538,16 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 break;
             }
 
+            EZ_T(3);
             // -- hash inserts of the visited lanes 0..last, last writer wins (writer.go:216-217)
             const int last = a < 0 ? nvalid - 1 : a;
             if (valid && lane <= last && next > last) {
                 ht[h] = (uint32_t)(start + x);
                 if (usefp) fp[h] = cur;
             }
-            if (valid) bmask[bk] = 0;
             __syncthreads();
 
+            EZ_T(4);
             if (a < 0) { i += nvalid; continue; }
 
             // -- lane a's action
@@ -520,12 +608,22 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                     done = ziend;
                 }
             }
+            EZ_T(5);
+#if (EZ_EXP & 64)
+            nev++;
+#endif
             // spec_mode 1: one emitting position resolved; K1x speculates again from here
             if (smode == 1 && i + 4 <= n && !o.err) {
                 stopped = true;
                 break;
             }
         }
+#if (EZ_EXP & 64)
+        if (lane == 0 && s == 0)
+            printf("K1 phases (cycles): refill+win %llu hash %llu eval %llu resolve %llu insert %llu action %llu; iters %llu events %llu\n",
+                   (unsigned long long)tph[0], (unsigned long long)tph[1], (unsigned long long)tph[2], (unsigned long long)tph[3],
+                   (unsigned long long)tph[4], (unsigned long long)tph[5], (unsigned long long)nit, (unsigned long long)nev);
+#endif
         if (stopped) {  // K1x's state back: the position, the pending literal, the output, the table
             if (lane == 0) A.spec[s] = SpecState{(uint32_t)i, (uint32_t)done, (uint32_t)o.op, 0u};
             if (HTL) for (int64_t k = lane; k < hs; k += kWave) A.spec_tab[s * (uint64_t)hs + k] = ht[k];
@@ -630,16 +728,23 @@ hipError_t launch_general(const CompressArgs &a, hipStream_t st) {
     if (pl) lds += ((a.max_len + 3) / 4 + 8) * 4;
     if (htl && !ring && !pl) lds += (size_t)a.hs * 16;  // candidate fingerprints
     lds = (lds + 15) & ~(size_t)15;
+    CompressArgs b = a;
+    b.win_bytes = 0;
+    if (!ring && !pl && !a.write_idx && a.max_len > (uint64_t)kPLdsMax) {  // long streams: the LDS window
+        static const uint32_t w = getenv("EZ_K1W_WIN") ? (uint32_t)atoi(getenv("EZ_K1W_WIN")) & ~15u : kWinBytes;
+        b.win_bytes = w;
+        if (w) lds += w + 32;
+    }
     uint64_t grid = a.count;
     if (!htl && !ring) grid = grid < 2048 ? grid : 2048;  // global scratch hash tables
     if (grid > (1u << 30)) grid = 1u << 30;
     const unsigned g = (unsigned)grid;
     if (pl) {
-        if (htl) return ring ? launch_variant<true, true, true>(a, st, lds, g) : launch_variant<true, true, false>(a, st, lds, g);
-        return ring ? launch_variant<true, false, true>(a, st, lds, g) : launch_variant<true, false, false>(a, st, lds, g);
+        if (htl) return ring ? launch_variant<true, true, true>(b, st, lds, g) : launch_variant<true, true, false>(b, st, lds, g);
+        return ring ? launch_variant<true, false, true>(b, st, lds, g) : launch_variant<true, false, false>(b, st, lds, g);
     }
-    if (htl) return ring ? launch_variant<false, true, true>(a, st, lds, g) : launch_variant<false, true, false>(a, st, lds, g);
-    return ring ? launch_variant<false, false, true>(a, st, lds, g) : launch_variant<false, false, false>(a, st, lds, g);
+    if (htl) return ring ? launch_variant<false, true, true>(b, st, lds, g) : launch_variant<false, true, false>(b, st, lds, g);
+    return ring ? launch_variant<false, false, true>(b, st, lds, g) : launch_variant<false, false, false>(b, st, lds, g);
 }
 
 }  // namespace ez

@@ -54,6 +54,7 @@ struct CompressArgs {
     uint32_t *spec_tab;
     SpecLit *spec_lit;
     uint32_t *spec_nlit;
+    uint32_t win_bytes;       // general kernel, long streams: LDS window bytes (set by its launcher)
 };
 
 

@@ -1,17 +1,7 @@
-#!/bin/bash
-# kernel-trace + stats profile of bench.py (args passed through) into gpurun_out/prof_$TAG
-set -o pipefail
-export TMPDIR=/tmp
-R=$GRAFT_REPO_ROOT
-TAG=${TAG:-run}
-mkdir -p $R/gpurun_out
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof_$TAG -o run -- python3 bench.py "$@" > $R/gpurun_out/prof_$TAG.log 2>&1
-rc=$?
-echo "prof $TAG rc=$rc"
-f=$(find $R/gpurun_out/prof_$TAG -name "*kernel_stats.csv" | head -1)
-[ -n "$f" ] && python3 -c "
-import csv,sys
-for r in csv.DictReader(open('$f')):
-    print(r['Name'][:60].ljust(60), r['Calls'], 'avg_ms=%.4f' % (float(r['AverageNs'])/1e6), 'pct=%s' % r['Percentage'])
-"
-exit $rc
+cd /tmp && export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/prof
+rm -rf $O && mkdir -p $O
+cd $GRAFT_REPO_ROOT
+for w in ${WLS:-c4 c4h c4s}; do
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$w -o run -- python3 bench.py --no-cpu --no-e2e --steps 3 --warmup 1 --workload $w > $O/$w.json 2> $O/$w.err || exit 1
+done

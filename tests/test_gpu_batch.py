@@ -338,8 +338,8 @@ def test_k1x_rounds(cuda, k1_kind):
     the rest after 8 rounds.  Planted matches at every distance up to past the window, runs,
     zero runs, the stream's first bytes, fewer and more events than rounds, empty and tiny
     streams beside long ones; block 1 MiB / 4 KiB / 1 KiB, tables 16 .. 4096 entries."""
-    if k1_kind not in ("", "x"):
-        pytest.skip("K1x's own shapes (the automatic choice and K1x forced)")
+    if k1_kind == "S":
+        pytest.skip("K1x's own shapes (automatic, K1x forced, and the general kernel alone with its LDS window)")
     from eazy_amd import synth
 
     rng = np.random.default_rng(41)
