@@ -1,16 +1,13 @@
 #!/bin/bash
-# PMC passes (one counter group per pass, no tracing domains mixed in)
-set -o pipefail
-R=$GRAFT_REPO_ROOT
-mkdir -p $R/gpurun_out/pmc
-export TMPDIR=/tmp
-rocprofv3 -L > $R/gpurun_out/pmc/counters.txt 2>&1 || true
-i=0
-for C in "${@}"; do
-  i=$((i+1))
-  timeout -k 10 300 rocprofv3 --pmc $C --output-format csv -d $R/gpurun_out/pmc/p$i -o run -- python3 bench.py --no-cpu --steps 2 --warmup 1 ${BENCH_ARGS:-} > $R/gpurun_out/pmc/p$i.log 2>&1
-  rc=$?
-  echo "pass $i rc=$rc: $C"
-  [ $rc -ne 0 ] && tail -5 $R/gpurun_out/pmc/p$i.log && exit $rc
+# PMC passes over one bench workload (one rocprofv3 run per counter set): bash gpurun_pmc.sh WORKLOAD "SET1" "SET2" ...
+cd /tmp && export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/pmc
+rm -rf $O && mkdir -p $O
+cd $GRAFT_REPO_ROOT
+W=$1; shift
+k=0
+for C in "$@"; do
+  k=$((k+1))
+  timeout -s KILL 120 rocprofv3 --pmc $C --output-format csv -d $O/p$k -o run -- python3 bench.py --no-cpu --no-e2e --no-gather --steps 2 --warmup 1 --workload $W > $O/p$k.log 2>&1 || { echo "pass $k failed"; tail -3 $O/p$k.log; exit 1; }
 done
-exit 0
+echo ok
