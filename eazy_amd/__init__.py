@@ -94,6 +94,7 @@ def _lib():
     L.ez_writer_set_append_magic.argtypes = [vp, C.c_int]
     L.ez_writer_set_version.argtypes = [vp, C.c_int]
     L.ez_writer_write.argtypes = [vp, C.c_char_p, sz, vp, sz, C.POINTER(sz)]
+    L.ez_writer_write_batch.argtypes = [vp, C.c_char_p, vp, sz, vp, sz, vp]
     L.ez_writer_header.argtypes = [vp, vp, sz, C.POINTER(sz)]
     L.ez_writer_break.argtypes = [vp, vp, sz, C.POINTER(sz)]
     L.ez_writer_reset.argtypes = [vp]
@@ -237,6 +238,7 @@ class Writer:
         self._ver = 0
         self._b = bytearray()
         self._written = 0
+        self._resets = 0
 
     def __del__(self):
         if getattr(self, "_h", None):
@@ -273,6 +275,39 @@ class Writer:
         self._write()
         return len(p)
 
+    def WriteBatch(self, ps) -> int:
+        """Several Writes in one device call (no reference counterpart; a throughput form of
+        Write for small Writes): the sink sees exactly what ``for p in ps: Write(p)`` gives it
+        — the same calls with the same bytes, FlushThreshold applied after each Write, the
+        first error raised — because the handle returns where each Write's bytes end and the
+        flushes are replayed per Write.  When a short sink write restarts the stream
+        (writer.go:391-393) the remaining Writes go through Write on the new stream.
+        Returns the bytes of all Writes."""
+        ps = [bytes(p) for p in ps]
+        k = len(ps)
+        if k == 0:
+            return 0
+        ends = (C.c_uint64 * k)()
+        at = 0
+        for j, p in enumerate(ps):
+            at += len(p)
+            ends[j] = at
+        cap = sum(compress_bound(len(p)) for p in ps)
+        buf = (C.c_uint8 * max(cap, 1))()
+        oe = (C.c_uint64 * k)()
+        _check(_lib().ez_writer_write_batch(self._h, b"".join(ps), ends, k, buf, cap, oe))
+        out = bytes(buf[: oe[k - 1]])
+        prev, gen = 0, self._resets
+        for j in range(k):
+            self._b += out[prev : oe[j]]
+            prev = oe[j]
+            self._write()
+            if self._resets != gen:  # the stream restarted: the rest on the new stream
+                for p in ps[j + 1 :]:
+                    self.Write(p)
+                break
+        return at
+
     def WriteHeader(self) -> None:  # writer.go:342-350
         if not _lib().ez_writer_is_reset(self._h):
             return
@@ -298,6 +333,7 @@ class Writer:
         self._written = 0
 
     def _reset(self) -> None:  # writer.go:187-200
+        self._resets += 1
         _check(_lib().ez_writer_reset(self._h))
         self._b = bytearray()
         self._written = 0

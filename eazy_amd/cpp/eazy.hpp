@@ -182,6 +182,37 @@ class Writer {
     std::pair<size_t, Err> Write(const std::vector<uint8_t> &p) { return Write(p.data(), p.size()); }
     std::pair<size_t, Err> Write(const std::string &p) { return Write((const uint8_t *)p.data(), p.size()); }
 
+    // k Writes in one device call (no reference counterpart): the sink sees what Write on each
+    // in turn gives it -- the handle returns where each Write's bytes end and FlushThreshold is
+    // replayed per Write; a short sink write that restarts the stream sends the remaining Writes
+    // through Write.  p holds the Writes back to back, Write j ending at p[ends[j]].
+    // {bytes of the Writes done, first error}.
+    std::pair<size_t, Err> WriteBatch(const uint8_t *p, const uint64_t *ends, size_t k) {
+        if (k == 0) return {0, Err::OK};
+        sync();
+        size_t cap = 0;
+        for (size_t j = 0; j < k; j++) cap += ez_compress_bound((size_t)(ends[j] - (j ? ends[j - 1] : 0)));
+        std::vector<uint8_t> tmp(cap ? cap : 1);
+        std::vector<uint64_t> oe(k);
+        const int st = ez_writer_write_batch(h_, p, ends, k, tmp.data(), cap, oe.data());
+        detail::panic_if(st, "eazy: WriteBatch");
+        if (st != EZ_OK) return {0, (Err)st};
+        const uint64_t gen = resets_;
+        for (size_t j = 0, prev = 0; j < k; prev = oe[j], j++) {
+            b_.insert(b_.end(), tmp.begin() + (ptrdiff_t)prev, tmp.begin() + (ptrdiff_t)oe[j]);
+            const Err e = write();
+            if (e != Err::OK) return {(size_t)(j ? ends[j - 1] : 0), e};
+            if (resets_ != gen) {  // the stream restarted: the rest on the new stream
+                for (size_t q = j + 1; q < k; q++) {
+                    auto [n, e2] = Write(p + ends[q - 1], (size_t)(ends[q] - ends[q - 1]));
+                    if (e2 != Err::OK) return {(size_t)ends[q - 1], e2};
+                }
+                break;
+            }
+        }
+        return {(size_t)ends[k - 1], Err::OK};
+    }
+
     Err WriteHeader() {  // writer.go:342-350
         if (!isreset()) return Err::OK;
         return append_call(ez_writer_header);
@@ -203,6 +234,7 @@ class Writer {
     ez_writer *h_ = nullptr;
     std::vector<uint8_t> b_;  // w.b
     int64_t written_ = 0;     // w.written
+    uint64_t resets_ = 0;     // stream restarts (WriteBatch's replay)
 
     void sync() {
         ez_writer_set_append_magic(h_, AppendMagic ? 1 : 0);
@@ -220,6 +252,7 @@ class Writer {
         return write();
     }
     void reset() {  // writer.go:187-200
+        resets_++;
         ez_writer_reset(h_);
         b_.clear();
         written_ = 0;

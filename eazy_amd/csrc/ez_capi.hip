@@ -191,6 +191,29 @@ extern "C" size_t ez_compress_bound(size_t n) { return (size_t)ez::compress_boun
 
 // ------------------------------------------------------------------ Writer handle
 
+// pinned host staging (one copy each way per call, no pageable bounce)
+struct HBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap) return EZ_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = n < 65536 ? 65536 : n + n / 4;
+        if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) return EZ_EDEVICE;
+        cap = c;
+        return EZ_OK;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T *as() const { return (T *)p; }
+};
+
 struct ez_writer {
     int device = 0;
     int64_t bs = 0, hs = 0;
@@ -198,7 +221,9 @@ struct ez_writer {
     int ver = 0;
     bool pristine = true;  // isreset(): nothing emitted since the last reset
     int64_t pos = 0;       // w.pos
-    DBuf ring, ht, in, out, meta;
+    // dev: [input | in_off[2] out_off[2] out_size status write_idx[2] | write_end[k] | write_out[k] | output]
+    DBuf ring, ht, dev;
+    HBuf host;             // the same layout, pinned
     hipStream_t stream = nullptr;
 };
 
@@ -249,9 +274,8 @@ extern "C" void ez_writer_free(ez_writer *w) {
     DeviceGuard g(w->device);
     w->ring.release();
     w->ht.release();
-    w->in.release();
-    w->out.release();
-    w->meta.release();
+    w->dev.release();
+    w->host.release();
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
 }
@@ -275,24 +299,41 @@ extern "C" int ez_writer_set_position(ez_writer *w, int64_t pos) {
     return EZ_OK;
 }
 
-extern "C" int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t *out, size_t cap, size_t *out_n) {
-    *out_n = 0;
-    const size_t bound = ez_compress_bound(n);
+namespace {
+
+// k Writes on the handle in one launch (k = 1: Writer.Write; k > 1: the same Writes in turn):
+// p holds them back to back, Write j ending at p[ends[j]]; out receives what each appends to
+// w.b, Write j's bytes ending at out[out_ends[j]].  One host->device copy (the Writes and the
+// launch metadata, from pinned staging), the general kernel with the handle's ring and table,
+// one device->host copy (status, sizes and bytes), one synchronisation.
+int writer_run(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, uint8_t *out, size_t cap, uint64_t *out_ends) {
+    const size_t n = k ? (size_t)ends[k - 1] : 0;
+    size_t bound = 0;
+    for (size_t j = 0; j < k; j++) {
+        if (ends[j] < (j ? ends[j - 1] : 0)) return EZ_EINVAL;
+        bound += ez_compress_bound((size_t)(ends[j] - (j ? ends[j - 1] : 0)));
+    }
     // checked before anything reaches the device: the kernel advances the handle's ring and table, so a
     // call that could not return its bytes must not run at all (a retry then sees the same history)
     if (cap < bound) return EZ_ENOSPC;
     DeviceGuard g(w->device);
     if (!g.ok) return EZ_EDEVICE;
-    if (w->in.ensure(n + 16) || w->out.ensure(bound + 16) || w->meta.ensure(64)) return EZ_EDEVICE;
-    // meta: in_off[2] out_off[2] out_size[1] status[1]
-    uint64_t m[6] = {0, (uint64_t)n, 0, (uint64_t)bound, 0, 0};
-    if (n) EZ_HIP(hipMemcpyAsync(w->in.p, p, n, hipMemcpyHostToDevice, w->stream));
-    EZ_HIP(hipMemcpyAsync(w->meta.p, m, sizeof(m), hipMemcpyHostToDevice, w->stream));
+    const size_t o_meta = (n + 15) & ~(size_t)15, nm = 8 + 2 * k;  // meta words
+    const size_t o_out = o_meta + nm * 8 + ((k > 1 ? k : 0) * 8);
+    const size_t total = ((o_out + 15) & ~(size_t)15) + bound + 16;
+    if (w->dev.ensure(total) || w->host.ensure(total)) return EZ_EDEVICE;
+    const size_t o_o = (o_out + 15) & ~(size_t)15;
+    uint8_t *H = w->host.as<uint8_t>(), *D = w->dev.as<uint8_t>();
+    if (n) memcpy(H, p, n);
+    uint64_t *m = (uint64_t *)(H + o_meta);
+    m[0] = 0; m[1] = n; m[2] = o_o; m[3] = o_o + bound; m[4] = 0; m[5] = 0; m[6] = 0; m[7] = k;
+    for (size_t j = 0; j < k; j++) m[8 + j] = ends[j];
+    EZ_HIP(hipMemcpyAsync(D, H, o_meta + nm * 8, hipMemcpyHostToDevice, w->stream));
+    uint64_t *dm = (uint64_t *)(D + o_meta);
     ez::CompressArgs a{};
-    uint64_t *dm = w->meta.as<uint64_t>();
-    a.in = w->in.as<uint8_t>();
+    a.in = D;
     a.in_off = dm;
-    a.out = w->out.as<uint8_t>();
+    a.out = D;
     a.out_off = dm + 2;
     a.out_size = dm + 4;
     a.status = (int32_t *)(dm + 5);
@@ -306,26 +347,51 @@ extern "C" int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t
     a.ring = w->ring.as<uint8_t>();
     a.ht_global = w->ht.as<uint32_t>();
     a.max_len = n ? n : 1;
+    if (k > 1) {  // the Writes' ends, and their output ends recorded by the kernel
+        a.write_idx = dm + 6;
+        a.write_end = dm + 8;
+        a.max_writes = k;
+        a.write_out = dm + 8 + k;
+    }
     EZ_HIP(ez::launch_compress(a, w->stream));
-    EZ_HIP(hipMemcpyAsync(m, w->meta.p, sizeof(m), hipMemcpyDeviceToHost, w->stream));
+    // status, sizes and output back at once (the bound, not the exact size: small Writes)
+    EZ_HIP(hipMemcpyAsync(H + o_meta, D + o_meta, o_o - o_meta + bound, hipMemcpyDeviceToHost, w->stream));
     EZ_HIP(hipStreamSynchronize(w->stream));
     int st = (int)(int32_t)(m[5] & 0xffffffffu);
     const size_t got = (size_t)m[4];
-    if (!st && got > cap) st = EZ_ENOSPC;  // cannot happen with cap >= bound (tests/test_bound.py)
+    if (!st && got > bound) st = EZ_ENOSPC;  // cannot happen (tests/test_bound.py)
     if (st) {
         // the device history already holds p while the stream position does not: start the stream
         // over, as Go does after a failed sink write (writer.go:391-393), so later Writes stay exact
         const int z = writer_zero(w);
         return z ? z : st;
     }
-    if (got) {
-        EZ_HIP(hipMemcpyAsync(out, w->out.p, got, hipMemcpyDeviceToHost, w->stream));
-        EZ_HIP(hipStreamSynchronize(w->stream));
+    if (got) memcpy(out, H + o_o, got);
+    if (out_ends) {
+        if (k > 1) for (size_t j = 0; j < k; j++) out_ends[j] = m[8 + k + j];
+        else if (k == 1) out_ends[0] = got;
     }
     w->pos += (int64_t)n;
     w->pristine = false;
-    *out_n = got;
     return EZ_OK;
+}
+
+}  // namespace
+
+extern "C" int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t *out, size_t cap, size_t *out_n) {
+    *out_n = 0;
+    const uint64_t end = n;
+    uint64_t oe = 0;
+    const int e = writer_run(w, p, &end, 1, out, cap, &oe);
+    if (!e) *out_n = (size_t)oe;
+    return e;
+}
+
+extern "C" int ez_writer_write_batch(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, uint8_t *out, size_t cap,
+                                     uint64_t *out_ends) {
+    if (k == 0) return EZ_OK;
+    if (!ends || !out_ends) return EZ_EINVAL;
+    return writer_run(w, p, ends, k, out, cap, out_ends);
 }
 
 extern "C" int ez_writer_header(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n) {

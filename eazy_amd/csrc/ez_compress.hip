@@ -160,10 +160,10 @@ template <bool PL, bool HTL, bool RING>
 __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem) {
     const int lane = lane_id();
     const uint64_t ib = A.in_off[s];
-    // multi-Write streams (A.write_idx, fresh streams only): Writes k = write_idx[s] ..
+    // multi-Write streams (A.write_idx; fresh streams, or the handle's stream with RING): Writes k = write_idx[s] ..
     // write_idx[s+1]-1 of one Writer, Write k ending at in[write_end[k]]; each Write's loop runs to
     // its own end (writer.go:213) and the table and the history carry over (writer.go:40-45)
-    const bool mw = !RING && A.write_idx != nullptr;
+    const bool mw = A.write_idx != nullptr;
     uint64_t wk = 0, wlast = 0;
     if (mw) {
         wk = A.write_idx[s];
@@ -274,7 +274,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     // Writes are the bytes before P.g in the same batch
     auto ringb = [&](int64_t y, int64_t wpos) -> uint32_t {
         const int64_t q = wpos - bs + ((y - wpos) & mask);
-        if (q >= start || (mw && q >= 0)) return P.b(q - start);
+        if (q >= start || (mw && q >= A.start)) return P.b(q - start);
         if (RING) return ring[q & mask];
         return 0u;
     };
@@ -294,8 +294,14 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         const int64_t r = (y - wpos) & mask;
         if (r + 7 >= bs) return false;  // wraps inside the 8 bytes
         const int64_t q = wpos - bs + r;
-        if (q >= start || (mw && q >= 0)) { v = s8(q - start); return true; }
-        if (!RING && q + 8 <= (mw ? 0 : start)) { v = 0; return true; }
+        if (q >= start || (mw && q >= A.start)) { v = s8(q - start); return true; }
+        if (!RING && q + 8 <= A.start) { v = 0; return true; }
+        // the handle's ring: bytes before this call, slot q & mask holds stream byte q (or the zero
+        // history); one 8-byte load instead of a dependent byte loop through HBM
+        if (RING && q + 8 <= A.start && (q & mask) + 8 <= bs) {
+            v = *(const uint64_t __attribute__((aligned(1))) *)(ring + (q & mask));
+            return true;
+        }
         return false;
     };
 
@@ -632,6 +638,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         // trailing literal (writer.go:324-329)
         if (!o.err && done < n) literal(done, n);
 
+        if (mw && A.write_out && lane == 0) A.write_out[wk] = (uint64_t)o.op;  // this Write's output ends here
         if (!mw || ++wk >= wlast || o.err) break;
         // the next Write: its bytes follow this one's in the batch
         start += n;
@@ -644,9 +651,10 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         P.glast = P.glast ? P.glast - 1 : 0;
     }
     if (RING) {
-        // copyData of this Write into the ring (writer.go:529-535), and
-        // the hash table back to HBM.
-        const int64_t k0 = n > bs ? n - bs : 0;
+        // copyData of this call's Writes into the ring (writer.go:529-535): the last bs bytes, the
+        // earlier Writes' bytes lying before the last one's in the batch; and the hash table back to HBM
+        int64_t k0 = n > bs ? n - bs : 0;
+        if (mw) k0 = n - bs > A.start - start ? n - bs : A.start - start;
         for (int64_t k = k0 + lane; k < n; k += kWave) A.ring[(start + k) & mask] = (uint8_t)P.b(k);
         if (HTL) for (int64_t k = lane; k < hs; k += kWave) A.ht_global[k] = ht[k];
     }

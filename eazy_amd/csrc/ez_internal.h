@@ -42,6 +42,7 @@ struct CompressArgs {
     const uint64_t *write_idx;
     const uint64_t *write_end;
     uint64_t max_writes;      // the most Writes of one stream (records reserved for their ends)
+    uint64_t *write_out;      // general kernel: the output size after each Write (nullptr: not recorded)
     // K1x rounds (ez_compress_spec.hip): the general kernel resumes a stream from K1x's state
     //   spec_mode 1: at spec_first[s] (streams with ~0u there are skipped), with the table
     //                spec_tab[s]; stops after the first accepted copy and stores its state back;

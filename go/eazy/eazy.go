@@ -128,6 +128,7 @@ type Writer struct {
 	h       *C.ez_writer
 	b       []byte
 	written int64
+	resets  uint64 // stream restarts (WriteBatch's replay)
 	ver     int
 }
 
@@ -224,7 +225,53 @@ func (w *Writer) ResetSize(wr io.Writer, block, htable int) {
 	w.written = 0
 }
 
-func (w *Writer) reset() { C.ez_writer_reset(w.h); w.b = w.b[:0]; w.written = 0 }
+func (w *Writer) reset() { w.resets++; C.ez_writer_reset(w.h); w.b = w.b[:0]; w.written = 0 }
+
+// WriteBatch compresses several Writes in one device call (no reference counterpart): the sink
+// sees what calling Write on each in turn gives it -- the handle reports where each Write's
+// bytes end and FlushThreshold is replayed per Write; a short sink write that restarts the
+// stream sends the remaining Writes through Write.  Returns the bytes of the Writes done.
+func (w *Writer) WriteBatch(ps [][]byte) (int, error) {
+	if len(ps) == 0 {
+		return 0, nil
+	}
+	w.sync()
+	var data []byte
+	ends := make([]uint64, len(ps))
+	need := 0
+	for j, p := range ps {
+		data = append(data, p...)
+		ends[j] = uint64(len(data))
+		need += int(C.ez_compress_bound(C.size_t(len(p))))
+	}
+	out := make([]byte, need+1)
+	oe := make([]uint64, len(ps))
+	st := C.ez_writer_write_batch(w.h, ptr(data), (*C.uint64_t)(unsafe.Pointer(&ends[0])), C.size_t(len(ps)),
+		ptr(out), C.size_t(need), (*C.uint64_t)(unsafe.Pointer(&oe[0])))
+	if st != C.EZ_OK {
+		return 0, toErr(st, 0)
+	}
+	gen, prev, done := w.resets, uint64(0), 0
+	for j := range ps {
+		w.b = append(w.b, out[prev:oe[j]]...)
+		prev = oe[j]
+		if err := w.write(); err != nil {
+			return done, err
+		}
+		done += len(ps[j])
+		if w.resets != gen { // the stream restarted: the rest on the new stream
+			for _, p := range ps[j+1:] {
+				n, err := w.Write(p)
+				done += n
+				if err != nil {
+					return done, err
+				}
+			}
+			break
+		}
+	}
+	return done, nil
+}
 
 func (w *Writer) isreset() bool { return int(w.written)+len(w.b) == 0 }
 

@@ -98,6 +98,15 @@ int ez_writer_set_version(ez_writer *w, int ver);     /* Writer.e.Ver writer.go:
  * out[0..*out_n) exactly the bytes Go appends to w.b for this call (header
  * included on a pristine stream).  cap >= ez_compress_bound(n). */
 int ez_writer_write(ez_writer *w, const uint8_t *p, size_t n, uint8_t *out, size_t cap, size_t *out_n);
+/* k Writes on the handle in one device call, the same as k ez_writer_write calls in
+ * turn: p holds the Writes back to back, Write j ending at p[ends[j]] (ends
+ * non-decreasing); out receives their bytes back to back, Write j's ending at
+ * out[out_ends[j]].  cap >= the sum of ez_compress_bound(len of Write j).  The
+ * mirrors replay FlushThreshold per Write from out_ends, so a caller batching small
+ * Writes sees the reference's sink calls (writer.go:379-401).  Errors as
+ * ez_writer_write (the stream restarts). */
+int ez_writer_write_batch(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, uint8_t *out, size_t cap,
+                          uint64_t *out_ends);
 int ez_writer_header(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n); /* WriteHeader writer.go:342 */
 int ez_writer_break(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n);  /* WriteBreak  writer.go:358 */
 int ez_writer_reset(ez_writer *w);                                          /* Reset       writer.go:149 (reset :187) */

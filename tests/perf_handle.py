@@ -57,6 +57,25 @@ def main():
         res[str(size)] = {"gpu_us_p50": float(np.median(lat)), "gpu_us_p99": float(np.percentile(lat, 99)),
                           "gpu_MiBps": size / (lat.mean() / 1e6) / 2**20,
                           "cpu_oracle_us": t_cpu * 1e6, "cpu_oracle_MiBps": size / t_cpu / 2**20}
+        # the same Writes in batches of 64 (ez_writer_write_batch: one launch per batch)
+        ends = (C.c_uint64 * 64)()
+        for j in range(64):
+            ends[j] = (j + 1) * size
+        bcap = 64 * cap
+        bbuf = (C.c_uint8 * bcap)()
+        oe = (C.c_uint64 * 64)()
+        assert L.ez_writer_new(1 << 20, 1024, 0, C.byref(h)) == 0
+        outs_b, blat = [], []
+        for j in range(0, len(ws) - 63, 64):
+            t0 = time.perf_counter()
+            assert L.ez_writer_write_batch(h, b"".join(ws[j : j + 64]), ends, 64, bbuf, bcap, oe) == 0
+            blat.append(time.perf_counter() - t0)
+            outs_b.append(bytes(bbuf[: oe[63]]))
+        L.ez_writer_free(h)
+        nb = len(outs_b) * 64
+        assert b"".join(outs_b) == b"".join(outs[:nb]), f"size {size}: batched bytes differ from the per-Write bytes"
+        res[str(size)]["batch64_us_per_write"] = float(np.mean(blat)) / 64 * 1e6
+        res[str(size)]["batch64_MiBps"] = 64 * size / float(np.mean(blat)) / 2**20
         # Reader.Read(4 KiB) loop over the stream
         r = ez.NewReaderBytes(gpu)
         got = bytearray()
@@ -71,7 +90,8 @@ def main():
         assert bytes(got) == b"".join(ws)
         res[str(size)]["reader_4k_MiBps"] = len(got) / t_r / 2**20
     print(json.dumps({"handle_path": res, "writes_per_size": a.writes,
-                      "note": "ez_writer_write per call: H2D copy, one wave-per-stream kernel, D2H copy, sync"}))
+                      "note": "ez_writer_write per call: one pinned H2D copy, the general kernel (a wave), one D2H copy, one sync; "
+                              "batch64: ez_writer_write_batch of 64 Writes per call"}))
 
 
 if __name__ == "__main__":

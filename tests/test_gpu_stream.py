@@ -354,3 +354,73 @@ def test_writer_positions_past_4gib(cuda):
         finally:
             L.ez_writer_free(h)
         assert b"".join(outs) == ow.sink, f"p0 = {p0:#x}"
+
+
+class _Sink:
+    """io.Writer recording every call; optionally one short write (the n-th call takes half)."""
+
+    def __init__(self, short_at=None):
+        self.calls, self.short_at = [], short_at
+
+    def write(self, b):
+        self.calls.append(bytes(b))
+        return len(b) // 2 if len(self.calls) == self.short_at else len(b)
+
+
+@pytest.mark.parametrize("block,ht,thr", [(1 << 20, 1024, 0), (1 << 20, 1024, 700), (4096, 64, -1), (1024, 32, 300), (2048, 16, 0)])
+def test_write_batch_equals_writes(cuda, block, ht, thr):
+    """Writer.WriteBatch (ez_writer_write_batch: k Writes in one launch on the handle's ring and
+    table, the general kernel's multi-Write path with the ring as older history) gives the sink
+    exactly the calls Write on each in turn gives it: ragged log Writes (empty, sub-hash, up to
+    3 KiB) in batches of 1..40, windows of 1 KiB .. 1 MiB (the ring wraps inside a batch), every
+    FlushThreshold regime; the stream equals the oracle's for the same Writes."""
+    import eazy_amd as ez
+    from eazy_amd import synth
+    import oracle as orc
+
+    rng = np.random.default_rng(block + ht + thr)
+    d = synth.logs(71, 1 << 20).tobytes()
+    writes, at = [], 0
+    for _ in range(400):
+        n = int(rng.choice([0, 1, 3, 4, 9, int(rng.integers(0, 400)), int(rng.integers(0, 3000))]))
+        writes.append(d[at : at + n])
+        at += n
+    sinks = []
+    for batched in (False, True):
+        s = _Sink()
+        w = ez.Writer(s, block, ht)
+        w.FlushThreshold = thr
+        j = 0
+        while j < len(writes):
+            k = int(rng.integers(1, 41)) if batched else 1
+            if batched:
+                assert w.WriteBatch(writes[j : j + k]) == sum(len(x) for x in writes[j : j + k])
+            else:
+                assert w.Write(writes[j]) == len(writes[j])
+            j += k
+        w.Flush()
+        sinks.append(s.calls)
+    assert sinks[1] == sinks[0]
+    assert b"".join(sinks[1]) == orc.compress(block, ht, writes)
+
+
+def test_write_batch_short_sink_write(cuda):
+    """A short sink write inside a batch restarts the stream (writer.go:387-401); the Writes after
+    it go to the new stream, as with Write one at a time."""
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    d = synth.logs(73, 1 << 16).tobytes()
+    writes = [d[k * 300 : (k + 1) * 300] for k in range(60)]
+    calls = []
+    for batched in (False, True):
+        s = _Sink(short_at=5)
+        w = ez.Writer(s, 1 << 20, 1024)
+        if batched:
+            w.WriteBatch(writes[:30])
+            w.WriteBatch(writes[30:])
+        else:
+            for p in writes:
+                w.Write(p)
+        calls.append(s.calls)
+    assert calls[1] == calls[0]
