@@ -407,6 +407,39 @@ static void TestBatchMatchesWriter() {  // the GPU batch path == one NewWriter(M
     for (void *p : {(void *)d_in, (void *)d_out, (void *)d_in_off, (void *)d_out_off, (void *)d_size, (void *)d_status}) (void)hipFree(p);
 }
 
+struct Recorder : IoWriter {  // an io.Writer keeping every call's bytes
+    std::vector<Bytes> calls;
+    std::pair<size_t, Err> Write(const uint8_t *p, size_t n) override {
+        calls.emplace_back(p, p + n);
+        return {n, Err::OK};
+    }
+};
+
+static void TestWriteBatch() {  // Writer::WriteBatch == Write on each in turn (same sink calls)
+    Bytes data;
+    std::vector<uint64_t> ends;
+    for (int j = 0; j < 120; j++) {
+        const int n = (j * 37) % 200;
+        for (int k = 0; k < n; k++) data.push_back((uint8_t)("ts=1 level=warn msg=\"disk\" "[(k * 3 + j) % 29]));
+        ends.push_back(data.size());
+    }
+    for (int thr : {0, 100, -1}) {
+        Recorder a, b;
+        auto wa = NewWriter(&a, 2048, 64), wb = NewWriter(&b, 2048, 64);
+        wa->FlushThreshold = wb->FlushThreshold = thr;
+        for (size_t j = 0; j < ends.size(); j++) write_ok(*wa, sub(data, j ? ends[j - 1] : 0, ends[j]));
+        for (size_t j = 0; j < ends.size(); j += 30) {  // batches of 30 Writes
+            std::vector<uint64_t> e;
+            const uint64_t base = j ? ends[j - 1] : 0;
+            for (size_t q = j; q < j + 30; q++) e.push_back(ends[q] - base);
+            auto [n, err] = wb->WriteBatch(data.data() + base, e.data(), e.size());
+            CHECK(err == Err::OK && n == e.back());
+        }
+        CHECK(wa->Flush() == Err::OK && wb->Flush() == Err::OK);
+        CHECK(a.calls == b.calls);
+    }
+}
+
 int main(int argc, char **argv) {
     const bool cpu = argc > 1 && std::string(argv[1]) == "--cpu";
     run("TestPrintLengthEncoding", TestPrintLengthEncoding);
@@ -434,6 +467,7 @@ int main(int argc, char **argv) {
         run("TestUnsupportedVersion", TestUnsupportedVersion);
         run("TestSinkFailureResets", TestSinkFailureResets);
         run("TestBatchMatchesWriter", TestBatchMatchesWriter);
+        run("TestWriteBatch", TestWriteBatch);
     }
     std::printf("%d/%d passed\n", g_run - g_fail, g_run);
     return g_fail ? 1 : 0;

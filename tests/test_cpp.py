@@ -30,4 +30,4 @@ def test_cpp_host_only():
 @pytest.mark.gpu
 def test_cpp_full(cuda):
     out = _run()
-    assert "FAIL" not in out and "20/20 passed" in out
+    assert "FAIL" not in out and "21/21 passed" in out
