@@ -83,9 +83,6 @@ struct InView {
     __device__ __forceinline__ uint32_t b(int64_t x) const {
         if (PL) return ((const uint8_t *)lw)[lr + (uint64_t)x];
         uint64_t a;
-#if (EZ_EXP & 32)
-        if (inw(x, 1, a) && ((const uint8_t *)ww)[a] != g[x]) printf("b mismatch x %lld a %llu wa0 %lld wnb %llu\n", (long long)x, (unsigned long long)a, (long long)wa0, (unsigned long long)wnb);
-#endif
         if (inw(x, 1, a)) return ((const uint8_t *)ww)[a];
         return g[x];
     }
@@ -233,17 +230,6 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         P.ww = (const uint32_t *)win;
         P.wa0 = a0;
         P.wnb = (uint64_t)n16 * 16;
-#if (EZ_EXP & 32)
-        for (int64_t k = lane; k < n16 * 16; k += kWave)
-            if (((const uint8_t *)win)[k] != ((const uint8_t *)src)[k]) printf("refill mismatch k %lld base %lld\n", (long long)k, (long long)base);
-        for (int64_t x = base + lane; x < base + 64; x += kWave) {
-            uint64_t wa;
-            if (P.inw(x, 16, wa)) {
-                const V16 v = P.wv16(wa), gv = ld16v(P.g + x);
-                if (v.lo != gv.lo || v.hi != gv.hi) printf("wv16 mismatch x %lld\n", (long long)x);
-            }
-        }
-#endif
     };
     // ---- hash table and bucket masks
     if (HTL) {
