@@ -153,14 +153,14 @@ __device__ __forceinline__ int64_t coop_count(int64_t from, int lane, F ok) {
     }
 }
 
-template <bool PL, bool HTL, bool RING>
+template <bool PL, bool HTL, bool RING, bool MWP>
 __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem) {
     const int lane = lane_id();
     const uint64_t ib = A.in_off[s];
     // multi-Write streams (A.write_idx; fresh streams, or the handle's stream with RING): Writes k = write_idx[s] ..
     // write_idx[s+1]-1 of one Writer, Write k ending at in[write_end[k]]; each Write's loop runs to
     // its own end (writer.go:213) and the table and the history carry over (writer.go:40-45)
-    const bool mw = A.write_idx != nullptr;
+    const bool mw = MWP && A.write_idx != nullptr;  // MWP: a multi-Write variant (fewer live scalars without)
     uint64_t wk = 0, wlast = 0;
     if (mw) {
         wk = A.write_idx[s];
@@ -651,26 +651,32 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     }
 }
 
-template <bool PL, bool HTL, bool RING>
+template <bool PL, bool HTL, bool RING, bool MWP>
 __global__ __launch_bounds__(64) void k1_compress(CompressArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     for (uint64_t s = blockIdx.x; s < A.count; s += gridDim.x) {
         // K1x resumes: finished streams, and in mode 1 the ones without an emitting position
         if (!RING && A.spec_mode && (A.spec[s].flags != 0 || (A.spec_mode == 1 && A.spec_first[s] == 0xffffffffu))) continue;
-        compress_stream<PL, HTL, RING>(A, s, smem);
+        compress_stream<PL, HTL, RING, MWP>(A, s, smem);
         __syncthreads();
     }
 }
 
-template <bool PL, bool HTL, bool RING>
-hipError_t launch_variant(const CompressArgs &a, hipStream_t st, size_t lds, unsigned grid) {
+template <bool PL, bool HTL, bool RING, bool MWP>
+hipError_t launch_variant_w(const CompressArgs &a, hipStream_t st, size_t lds, unsigned grid) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_compress<PL, HTL, RING>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_compress<PL, HTL, RING, MWP>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
-    hipLaunchKernelGGL((k1_compress<PL, HTL, RING>), dim3(grid), dim3(64), lds, st, a);
+    hipLaunchKernelGGL((k1_compress<PL, HTL, RING, MWP>), dim3(grid), dim3(64), lds, st, a);
     return hipGetLastError();
+}
+template <bool PL, bool HTL, bool RING>
+hipError_t launch_variant(const CompressArgs &a, hipStream_t st, size_t lds, unsigned grid) {
+    // PL excludes multi-Write streams (the launcher), so its variants need no multi-Write code
+    if (!PL && a.write_idx) return launch_variant_w<PL, HTL, RING, true>(a, st, lds, grid);
+    return launch_variant_w<PL, HTL, RING, false>(a, st, lds, grid);
 }
 
 }  // namespace
