@@ -26,6 +26,7 @@
 //   q = w.pos - bs + ((x - w.pos) mod bs);  byte = q >= start ? p[q-start]
 //                                                  : (ring ? ring[q & mask] : 0)
 #include <string>
+#include <type_traits>
 
 #include "ez_format.h"
 #include "ez_internal.h"
@@ -143,18 +144,22 @@ __device__ __forceinline__ void put_literal(OutBuf &o, const V &P, int64_t st, i
 }
 
 // Wave-cooperative extension: number of consecutive m >= from with ok(m).
-template <class F>
-__device__ __forceinline__ int64_t coop_count(int64_t from, int lane, F ok) {
-    int64_t base = from;
+template <class T, class F>
+__device__ __forceinline__ T coop_count(T from, int lane, F ok) {
+    T base = from;
     for (;;) {
-        const uint64_t bad = wballot(!ok(base + lane));
-        if (bad) return base + ffs64(bad);
+        const uint64_t bad = wballot(!ok(base + (T)lane));
+        if (bad) return base + (T)ffs64(bad);
         base += kWave;
     }
 }
 
 template <bool PL, bool HTL, bool RING, bool MWP>
 __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem) {
+    // SMALL (fresh single-Write streams shorter than 2 GiB: the launcher's non-multi-Write, non-ring
+    // variants): stream positions in 32 bits and start = 0 -- fewer live scalars, 32-bit math
+    constexpr bool SMALL = !RING && !MWP;
+    typedef typename std::conditional<SMALL, int32_t, int64_t>::type I;
     const int lane = lane_id();
     const uint64_t ib = A.in_off[s];
     // multi-Write streams (A.write_idx; fresh streams, or the handle's stream with RING): Writes k = write_idx[s] ..
@@ -167,11 +172,11 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         wlast = A.write_idx[s + 1];
     }
     uint64_t wbeg = ib;  // the current Write's first byte (index into A.in)
-    int64_t n = (int64_t)((mw ? (wk < wlast ? A.write_end[wk] : ib) : A.in_off[s + 1]) - ib);
+    I n = (I)((mw ? (wk < wlast ? A.write_end[wk] : ib) : A.in_off[s + 1]) - ib);
     const int64_t bs = A.bs, mask = bs - 1;
-    const int64_t hs = A.hs;
+    const I hs = A.hs;
     const unsigned hsh = 32u - (unsigned)(64 - __builtin_clzll((uint64_t)(hs - 1)));
-    int64_t start = A.start;  // stream position of the current Write's first byte
+    I start = SMALL ? (I)0 : (I)A.start;  // stream position of the current Write's first byte (fresh single Writes: 0)
     const uint8_t *ring = A.ring;
 
     // ---- LDS carve (all offsets 16-aligned)
@@ -210,7 +215,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     const bool wl = !PL && !RING && !mw && A.win_bytes != 0 && smode != 1 && A.in_off[A.count] >= 16;
     bool wend = false;  // the window reaches the stream's (or the batch's) end: no later refill
     // window from stream position base (16-byte aligned addresses, inside the batch)
-    auto refill = [&](int64_t base) {
+    auto refill = [&](I base) {
         const uint64_t ga = (uint64_t)(uintptr_t)P.gw;
         int64_t a0 = (int64_t)(((ga + P.gr + (uint64_t)base) & ~15ull) - ga);
         if (ga + (uint64_t)a0 < (uint64_t)(uintptr_t)P.lo) a0 += 16;
@@ -224,7 +229,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         __syncthreads();  // the old window's readers are done
         const uint4 *src = (const uint4 *)(ga + (uint64_t)a0);
 #pragma unroll 8
-        for (int64_t k = lane; k < n16; k += kWave) win[k] = src[k];
+        for (I k = lane; k < n16; k += kWave) win[k] = src[k];
         if (lane < 2) win[n16 + lane] = make_uint4(0, 0, 0, 0);
         __syncthreads();
         P.ww = (const uint32_t *)win;
@@ -233,11 +238,11 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     };
     // ---- hash table and bucket masks
     if (HTL) {
-        if (RING) for (int64_t k = lane; k < hs; k += kWave) ht[k] = A.ht_global[k];
-        else if (smode) for (int64_t k = lane; k < hs; k += kWave) ht[k] = A.spec_tab[s * (uint64_t)hs + k];
-        else for (int64_t k = lane; k < hs; k += kWave) ht[k] = 0;
+        if (RING) for (I k = lane; k < hs; k += kWave) ht[k] = A.ht_global[k];
+        else if (smode) for (I k = lane; k < hs; k += kWave) ht[k] = A.spec_tab[s * (uint64_t)hs + k];
+        else for (I k = lane; k < hs; k += kWave) ht[k] = 0;
     } else if (!RING) {
-        for (int64_t k = lane; k < hs; k += kWave) ht[k] = 0;
+        for (I k = lane; k < hs; k += kWave) ht[k] = 0;
     }
     __syncthreads();
 
@@ -258,7 +263,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
 
     // block[y & mask] as seen while w.pos == wpos; a multi-Write stream's earlier
     // Writes are the bytes before P.g in the same batch
-    auto ringb = [&](int64_t y, int64_t wpos) -> uint32_t {
+    auto ringb = [&](I y, I wpos) -> uint32_t {
         const int64_t q = wpos - bs + ((y - wpos) & mask);
         if (q >= start || (mw && q >= A.start)) return P.b(q - start);
         if (RING) return ring[q & mask];
@@ -269,14 +274,14 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     // and the 8 bytes block[(y .. y+7) & mask] when they map to 8 consecutive stream
     // bytes or to the zero history before a fresh stream (false: take the byte loop)
     const uint8_t *in_lo = A.in, *in_hi = A.in + A.in_off[A.count];
-    auto s8 = [&](int64_t y) -> uint64_t {
+    auto s8 = [&](I y) -> uint64_t {
         uint64_t wa;
         if (P.inw(y, 8, wa)) return P.wv16(wa).lo;
         const uint8_t *q = P.g + y;
         if (q >= in_lo && q + 8 <= in_hi) return *(const uint64_t __attribute__((aligned(1))) *)q;
         return (in_hi - in_lo >= 16) ? ld_clamped(q, in_lo, in_hi).lo : 0ull;
     };
-    auto ring8 = [&](int64_t y, int64_t wpos, uint64_t &v) -> bool {
+    auto ring8 = [&](I y, I wpos, uint64_t &v) -> bool {
         const int64_t r = (y - wpos) & mask;
         if (r + 7 >= bs) return false;  // wraps inside the 8 bytes
         const int64_t q = wpos - bs + r;
@@ -293,7 +298,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
 
     // appendLiteral; in spec_mode 1 the bytes are left to K1x's copy kernel (a literal there can be
     // megabytes, one wave would copy it at 1 KiB per step)
-    auto literal = [&](int64_t st, int64_t end) {
+    auto literal = [&](I st, I end) {
         if (smode != 1) { put_literal(o, P, st, end, lane); return; }
         Hdr h;
         if (!hdr_tag(h, kLiteral, end - st)) { o.err = EZ_EINVAL; return; }
@@ -305,29 +310,29 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     };
     bool stopped = false;  // spec_mode 1: stopped after one accepted copy
     for (;;) {  // the stream's Writes (one unless mw)
-        int64_t done = smode ? (int64_t)A.spec[s].done : 0;
-        int64_t i = smode == 1 ? (int64_t)A.spec_first[s] : (smode == 2 ? (int64_t)A.spec[s].from : 0);
+        I done = smode ? (I)A.spec[s].done : 0;
+        I i = smode == 1 ? (I)A.spec_first[s] : (smode == 2 ? (I)A.spec[s].from : 0);
         int64_t guard = 0;
         const int64_t guard_max = 16 * n + 4096;
         // global input: the 16 bytes x-8 .. x+7 around each lane's position, and those of
         // the window after this one if nothing is accepted (loaded while this one is judged)
         const bool pf = !PL && in_hi - in_lo >= 16;
-        auto around = [&](int64_t y) -> V16 {
+        auto around = [&](I y) -> V16 {
             uint64_t wa;
             if (P.inw(y - 8, 16, wa)) return P.wv16(wa);
             const uint8_t *q = P.g + y - 8;
             return q >= in_lo && q + 16 <= in_hi ? ld16v(q) : ld_clamped(q, in_lo, in_hi);
         };
         V16 nxt_w{0, 0};
-        int64_t nxt_i = -1;
+        I nxt_i = -1;
         const bool usefp = FP && pf && start == 0 && smode != 1;
         if (usefp) {
             if (smode == 2) {  // K1x's table: the bytes around each entry's position
 #pragma unroll 4
-                for (int64_t k = lane; k < hs; k += kWave) fp[k] = around((int64_t)ht[k]);
+                for (I k = lane; k < hs; k += kWave) fp[k] = around((I)ht[k]);
             } else {  // the zero entries hold stream position 0
                 const V16 z = around(0);
-                for (int64_t k = lane; k < hs; k += kWave) fp[k] = z;
+                for (I k = lane; k < hs; k += kWave) fp[k] = z;
             }
             __syncthreads();
         }
@@ -350,16 +355,20 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                     refill(i > 512 ? i - 512 : 0);
                 }
             }
-            const int64_t wpos = start + done;
-            const int64_t rem = n - 3 - i;
+            const I wpos = start + done;
+            const I rem = n - 3 - i;
             const int nvalid = rem < kWave ? (int)rem : kWave;
-            const int64_t x = i + lane;
+            const I x = i + lane;
             const bool valid = lane < nvalid;
             V16 cur{0, 0};  // bytes x-8 .. x+7 (pf)
             if (pf) {
-                cur = nxt_i == i ? nxt_w : around(x);
-                nxt_w = around(x + nvalid);
-                nxt_i = i + nvalid;
+                if (wl) {  // LDS window: no prefetch (an LDS read is short)
+                    cur = around(x);
+                } else {
+                    cur = nxt_i == i ? nxt_w : around(x);
+                    nxt_w = around(x + nvalid);
+                    nxt_i = i + nvalid;
+                }
             }
 
             EZ_T(0);
@@ -381,8 +390,8 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 if (below) prev = 63 - __builtin_clzll(below);
                 if (above) next = __builtin_ctzll(above);
             }
-            int64_t cand = 0;
-            if (valid) cand = prev >= 0 ? (int64_t)(uint32_t)(start + i + prev) : (int64_t)ht[h];
+            I cand = 0;
+            if (valid) cand = prev >= 0 ? (I)(uint32_t)(start + i + prev) : (I)ht[h];
             // the candidate's bytes cand-8 .. cand+7 (usefp): an earlier lane's, or the table's
             V16 cv{0, 0};
             if (usefp) {
@@ -395,14 +404,14 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
             // -- per-lane capped evaluation
             int kind = kReject;
             bool exact = true;
-            int64_t v_st = 0, v_ist = 0, v_iend = 0;
+            I v_st = 0, v_ist = 0, v_iend = 0;
             if (valid) {
-                const int64_t off = cand - wpos;
+                const I off = cand - wpos;
                 if (-off > bs) {
                     kind = kReject;  // far skip (writer.go:221-224)
                 } else if (off >= 0 && x > done + off) {
                     // runlen (writer.go:227-231 -> writeRunlen :441-489)
-                    const int64_t st = done + off;
+                    const I st = done + off;
                     v_st = st;
                     if (st + 8 < n && (usefp ? cv.hi == 0 : (P.u32(st) == 0 && P.u32(st + 4) == 0))) {
                         kind = kZero;
@@ -414,7 +423,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                             f = df ? (int)(__builtin_ctzll(df) >> 3) : 8;
                             if (f > n - x) f = (int)(n - x);
                             c = db ? (int)(__builtin_clzll(db) >> 3) : 8;
-                            const int64_t cl = st < x - done ? st : x - done;
+                            const I cl = st < x - done ? st : x - done;
                             if (c > cl) c = (int)cl;
                         } else {
                             while (f < kCap && x + f < n && P.b(st + f) == P.b(x + f)) f++;
@@ -427,7 +436,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                     }
                 } else {
                     // window match (writer.go:233-301)
-                    int64_t ist = x - 1, st = cand - 1;
+                    I ist = x - 1, st = cand - 1;
                     int c = 0;
                     uint64_t rb = 0, rf = 0;
                     bool vec;
@@ -448,7 +457,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                         while (c < kCap && ist >= done && P.b(ist) == ringb(st, wpos)) { ist--; st--; c++; }
                     }
                     ist++; st++;
-                    int64_t iend = x, end = cand;
+                    I iend = x, end = cand;
                     int f = 0;
                     if (vec) {
                         const uint64_t df = (pf ? cur.hi : s8(x)) ^ rf;
@@ -477,29 +486,29 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
             uint64_t cm = wballot(valid && kind != kReject);
             const uint64_t exm = wballot(exact);
             int a = -1, ka = kReject;
-            int64_t xa = 0, sta = 0, ista = 0, ienda = 0, canda = 0;
+            I xa = 0, sta = 0, ista = 0, ienda = 0, canda = 0;
             while (cm) {
                 const int l = ffs64(cm);
                 const int kl = rl32(kind, l);
                 const bool ex = (exm >> l) & 1;
-                const int64_t xl = i + l;
+                const I xl = i + l;
                 if (kl == kWin) {
-                    const int64_t cl = rl64(cand, l);
-                    int64_t ist, iend;
+                    const I cl = rl64(cand, l);
+                    I ist, iend;
                     if (ex) {
                         ist = rl64(v_ist, l);
                         iend = rl64(v_iend, l);
                     } else {
-                        const int64_t bw = coop_count(0, lane, [&](int64_t m) {
+                        const I bw = coop_count((I)0, lane, [&](I m) {
                             return xl - 1 - m >= done && P.b(xl - 1 - m) == ringb(cl - 1 - m, wpos);
                         });
-                        const int64_t fw = coop_count(0, lane, [&](int64_t m) {
+                        const I fw = coop_count((I)0, lane, [&](I m) {
                             return xl + m < n && P.b(xl + m) == ringb(cl + m, wpos);
                         });
                         ist = xl - bw;
-                        int64_t st = cl - bw;
+                        I st = cl - bw;
                         iend = xl + fw;
-                        int64_t end = cl + fw;
+                        I end = cl + fw;
                         const int64_t blit = wpos - bs;
                         const int64_t bend = blit + (iend - done);
                         int64_t d = bend - st;
@@ -517,10 +526,10 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                         ista = rl64(v_ist, l);
                         ienda = rl64(v_iend, l);
                     } else {
-                        const int64_t jf = coop_count(0, lane, [&](int64_t m) {
+                        const I jf = coop_count((I)0, lane, [&](I m) {
                             return xl + m < n && P.b(sta + m) == P.b(xl + m);
                         });
-                        const int64_t jb = coop_count(0, lane, [&](int64_t m) {
+                        const I jb = coop_count((I)0, lane, [&](I m) {
                             return sta - 1 - m >= 0 && xl - 1 - m >= done && P.b(sta - 1 - m) == P.b(xl - 1 - m);
                         });
                         ista = xl - jb;
@@ -546,8 +555,8 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
             if (ka == kWin) {
                 // writer.go:303-321
                 if (done < ista) literal(done, ista);
-                const int64_t dist = start + xa - canda;  // w.pos - st after the literal
-                const int64_t L = ienda - ista;
+                const I dist = start + xa - canda;  // w.pos - st after the literal
+                const I L = ienda - ista;
                 if (dist > bs) { o.err = EZ_EINVAL; break; }  // panic("too big offset")
                 Hdr hh;
                 if (!hdr_tag(hh, kCopy, L) || !hdr_offset(hh, dist, L)) { o.err = EZ_EINVAL; break; }
@@ -578,15 +587,15 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
                 done = ienda;
             } else if (ka == kCut) {
                 // writer.go:464-473
-                const int64_t iend = done + xa - sta;
+                const I iend = done + xa - sta;
                 literal(done, iend);
                 i = iend;
                 done = iend;
             } else {
                 // writeZeros writer.go:407-439, called with i = st
-                const int64_t zf = coop_count(0, lane, [&](int64_t m) { return sta + m < n && P.b(sta + m) == 0; });
-                const int64_t zb = coop_count(0, lane, [&](int64_t m) { return sta - 1 - m >= done && P.b(sta - 1 - m) == 0; });
-                const int64_t zi = sta - zb, ziend = sta + zf;
+                const I zf = coop_count((I)0, lane, [&](I m) { return sta + m < n && P.b(sta + m) == 0; });
+                const I zb = coop_count((I)0, lane, [&](I m) { return sta - 1 - m >= done && P.b(sta - 1 - m) == 0; });
+                const I zi = sta - zb, ziend = sta + zf;
                 if (ziend - zi < kMinCopyChunk) {
                     i = zi + 1;  // unreachable: >= 8 zeros are guaranteed
                 } else {
@@ -618,7 +627,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
 #endif
         if (stopped) {  // K1x's state back: the position, the pending literal, the output, the table
             if (lane == 0) A.spec[s] = SpecState{(uint32_t)i, (uint32_t)done, (uint32_t)o.op, 0u};
-            if (HTL) for (int64_t k = lane; k < hs; k += kWave) A.spec_tab[s * (uint64_t)hs + k] = ht[k];
+            if (HTL) for (I k = lane; k < hs; k += kWave) A.spec_tab[s * (uint64_t)hs + k] = ht[k];
             return;
         }
         // trailing literal (writer.go:324-329)
@@ -629,7 +638,7 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
         // the next Write: its bytes follow this one's in the batch
         start += n;
         wbeg = A.write_end[wk - 1];
-        n = (int64_t)(A.write_end[wk] - wbeg);
+        n = (I)(A.write_end[wk] - wbeg);
         P.g = A.in + wbeg;
         P.gr = (uint64_t)(uintptr_t)P.g & 3;
         P.gw = (const uint32_t *)(P.g - P.gr);
@@ -639,10 +648,10 @@ __device__ void compress_stream(const CompressArgs &A, uint64_t s, uint8_t *smem
     if (RING) {
         // copyData of this call's Writes into the ring (writer.go:529-535): the last bs bytes, the
         // earlier Writes' bytes lying before the last one's in the batch; and the hash table back to HBM
-        int64_t k0 = n > bs ? n - bs : 0;
+        I k0 = n > bs ? n - bs : 0;
         if (mw) k0 = n - bs > A.start - start ? n - bs : A.start - start;
-        for (int64_t k = k0 + lane; k < n; k += kWave) A.ring[(start + k) & mask] = (uint8_t)P.b(k);
-        if (HTL) for (int64_t k = lane; k < hs; k += kWave) A.ht_global[k] = ht[k];
+        for (I k = k0 + lane; k < n; k += kWave) A.ring[(start + k) & mask] = (uint8_t)P.b(k);
+        if (HTL) for (I k = lane; k < hs; k += kWave) A.ht_global[k] = ht[k];
     }
     if (lane == 0) {
         A.out_size[s] = (uint64_t)o.op;
@@ -675,7 +684,8 @@ hipError_t launch_variant_w(const CompressArgs &a, hipStream_t st, size_t lds, u
 template <bool PL, bool HTL, bool RING>
 hipError_t launch_variant(const CompressArgs &a, hipStream_t st, size_t lds, unsigned grid) {
     // PL excludes multi-Write streams (the launcher), so its variants need no multi-Write code
-    if (!PL && a.write_idx) return launch_variant_w<PL, HTL, RING, true>(a, st, lds, grid);
+    // (and the 64-bit-position code for fresh Writes of 2 GiB or more: SMALL needs < 2^31)
+    if (!PL && (a.write_idx || a.max_len >= (1ull << 31) || a.max_len == 0)) return launch_variant_w<PL, HTL, RING, true>(a, st, lds, grid);
     return launch_variant_w<PL, HTL, RING, false>(a, st, lds, grid);
 }
 
