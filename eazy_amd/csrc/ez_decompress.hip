@@ -241,7 +241,10 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
 static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'r', 'w'
 void select_decompress_variant(int v) { g_decompress_variant = v; }
 
-uint64_t decompress_workspace_words(uint64_t count) { return 2 * count + 32; }
+// [slow list: 2 * count + 32 words][K2w's deferred literals: 4 words + count * kDefSlots records]
+uint64_t decompress_workspace_words(uint64_t count) {
+    return 2 * count + 32 + 4 + count * (uint64_t)kDefSlots * (sizeof(DeferLit) / 4);
+}
 
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;
@@ -268,12 +271,19 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     }
     if (g_decompress_variant == 'w' || (g_decompress_variant == 0 && a.max_out >= long_slot)) {
         // long streams (slots of 64 KiB and more, C2/C4): too few to give every lane one;
-        // K2w gives each a wave, and its hand-overs go to the exact decoder
-        e = launch_decompress_wave(a, st);
+        // K2w gives each a wave, and its hand-overs go to the exact decoder; the long literals
+        // it defers are moved last (the exact decoder writes the same bytes for a stream it takes)
+        DecompressArgs b = a;
+        static const bool no_defer = getenv("EZ_K2W_DEFER") && atoi(getenv("EZ_K2W_DEFER")) == 0;  // A/B
+        b.defer = no_defer ? nullptr : a.slow + 2 * a.count + 32;
+        b.defer_cap = a.count * (uint64_t)kDefSlots;
+        if (b.defer && (e = hipMemsetAsync(b.defer, 0, 16, st)) != hipSuccess) return e;
+        e = launch_decompress_wave(b, st);
         if (e != hipSuccess) return e;
         const uint64_t grid = a.count < 4096 ? a.count : 4096;
         hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
-        return hipGetLastError();
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return b.defer ? launch_defer_copy(b, st) : hipSuccess;
     }
     // K2r (default): one lane per stream with the recent output in an LDS ring
     e = launch_decompress_ring(a, st);

@@ -29,6 +29,11 @@ constexpr int32_t kWIn = 1024;     // input ring bytes per stream (power of two)
 constexpr int32_t kWStage = 512;   // input staged this many bytes at a time (32 lanes x 16)
 constexpr int32_t kWChunk = 1024;  // output leaves the ring this many bytes at a time
 constexpr size_t kWLds = 16 + (size_t)kWR + 32 + kWIn + 16;
+// Long literals (C4: a whole fp32 bucket is one literal) are not moved through the ring by the
+// stream's one wave (1 KiB per pass, one HBM round trip each): their tag is parsed, the ring gets
+// their last 8 KiB, and kd_copy moves their bytes with the whole chip afterwards.  A far copy
+// reading from such a literal before kd_copy has run reads its bytes from the input instead.
+constexpr int32_t kDeferMin = 16384;  // literals this long are deferred
 
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 
@@ -74,6 +79,28 @@ __device__ __forceinline__ V16 ld_in(const uint8_t *y, const uint8_t *lo, const 
     return y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
 }
 
+// the 16 output bytes at sq (< the ring's reach) from HBM, or from the input where they lie in a
+// deferred literal (dd/ds/dl: its output position, input position, length; nd of them)
+__device__ __forceinline__ V16 far16(const uint8_t *out, int32_t cap, const uint8_t *b, int32_t sq, int nd, const int32_t *dd,
+                                     const int32_t *ds, const int32_t *dl) {
+    bool hit = false;
+#pragma unroll
+    for (int k = 0; k < kDefSlots; k++)
+        if (k < nd && sq < dd[k] + dl[k] && sq + 16 > dd[k]) hit = true;
+    if (!hit) return sq >= 0 ? ld16v(out + sq) : ld_clamped(out + sq, out, out + cap);
+    V16 v{0, 0};
+    for (int t = 0; t < 16; t++) {
+        const int32_t y = sq + t;
+        uint64_t c = y >= 0 ? out[y] : 0;
+#pragma unroll
+        for (int k = 0; k < kDefSlots; k++)
+            if (k < nd && y >= dd[k] && y < dd[k] + dl[k]) c = b[ds[k] + (y - dd[k])];
+        if (t < 8) v.lo |= c << (8 * t);
+        else v.hi |= c << (8 * (t - 8));
+    }
+    return v;
+}
+
 // stream s by the whole wave; false = hand it over
 __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring, uint8_t *inb, const int lane) {
     const uint8_t *b = A.in + A.in_off[s];
@@ -107,7 +134,11 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
     for (; in_hi < kWIn; in_hi += kWStage) put_in(in_hi, get_in(in_hi));
     V16 pend = get_in(in_hi);
 
-    int32_t i = 0, pos = 0, bsl = -1, fl = 0;  // fl: output below it is in HBM
+    int32_t i = 0, pos = 0, bsl = -1, fl = 0;  // fl: output below it is in HBM (or deferred)
+    int nd = 0;                                 // deferred literals of this stream
+    int32_t dd[kDefSlots], ds[kDefSlots], dl[kDefSlots];
+#pragma unroll
+    for (int k = 0; k < kDefSlots; k++) dd[k] = ds[k] = dl[k] = 0;
     // A group: tokens whose sources lie before the group's first output byte gpos
     // (literals staged in the input ring, copies with D >= L from the output ring),
     // cut into pieces of <= 16 bytes, one per lane: one LDS read and one exact write
@@ -241,6 +272,32 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
                 }
                 used += np;
                 pos += L;
+            } else if (r == kParseToken && !t.cp && L >= kDeferMin && nd < kDefSlots && A.defer) {
+                // a long literal: the bytes before it leave the ring exactly, the ring gets its last
+                // kWR bytes, kd_copy moves it (the record's slot from the batch-wide counter)
+                run_group();
+                for (int32_t q = fl + 16 * lane; q < pos; q += 1024) {
+                    const V16 v = rld<kWR>(ring, q);
+                    if (q + 16 <= pos) st16v(out + q, v);
+                    else put_small(out + q, v, (uint32_t)(pos - q));
+                }
+                const int32_t tail = L - kWR;  // >= 0: kDeferMin > kWR
+#pragma unroll
+                for (int32_t k = 0; k < kWR / 1024; k++) {
+                    const int32_t q = tail + 1024 * k + 16 * lane;
+                    rst<kWR>(ring, pos + q, ld_in(b + src + q, A.in, in_end));
+                }
+                if (lane == 0) {
+                    const uint32_t at = atomicAdd(&A.defer[0], 1u);
+                    if (at < A.defer_cap) ((DeferLit *)(A.defer + 4))[at] = DeferLit{A.in_off[s] + (uint64_t)src, A.out_off[s] + (uint64_t)pos, (uint64_t)L};
+                }
+#pragma unroll
+                for (int k = 0; k < kDefSlots; k++)
+                    if (k == nd) { dd[k] = pos; ds[k] = src; dl[k] = L; }
+                nd++;
+                pos += L;
+                fl = pos;
+                gpos = pos;
             } else if (r == kParseToken) {
                 run_group();
                 const int32_t D = (int32_t)t.D;
@@ -267,7 +324,7 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
                     if (act) {
                         V16 v = pv;
                         if (!t.cp) v = staged ? rld<kWIn>(inb, src + q) : ld_in(b + src + q, A.in, in_end);
-                        else if (D >= 16) v = sq >= rlo ? rld<kWR>(ring, sq) : (sq >= 0 ? ld16v(out + sq) : ld_clamped(out + sq, out, out + cap));
+                        else if (D >= 16) v = sq >= rlo ? rld<kWR>(ring, sq) : far16(out, cap, b, sq, nd, dd, ds, dl);
                         rst<kWR>(ring, pos + q, v);
                     }
                     const int32_t fin = pos + (done + W < L ? done + W : L);  // final bytes end here
@@ -307,7 +364,33 @@ __global__ __launch_bounds__(64) void k2_wave(DecompressArgs A) {
         }
 }
 
+// every deferred literal's bytes, 64 KiB per block step
+__global__ __launch_bounds__(256) void kd_copy(DecompressArgs A, uint64_t kp) {
+    const uint64_t nl = A.defer[0] < A.defer_cap ? A.defer[0] : A.defer_cap;
+    const DeferLit *rec = (const DeferLit *)(A.defer + 4);
+    const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
+    for (uint64_t q = blockIdx.x; q < nl * kp; q += gridDim.x) {
+        const DeferLit L = rec[q / kp];
+        const uint64_t b = (q % kp) * 65536;
+        if (b >= L.len) continue;
+        const uint64_t e = b + 65536 < L.len ? b + 65536 : L.len;
+        for (uint64_t k = b + 16 * threadIdx.x; k < e; k += 16 * 256) {
+            const uint8_t *y = A.in + L.src + k;
+            const V16 v = y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
+            if (k + 16 <= e) st16v(A.out + L.dst + k, v);
+            else put_small(A.out + L.dst + k, v, (uint32_t)(e - k));
+        }
+    }
+}
+
 }  // namespace
+
+hipError_t launch_defer_copy(const DecompressArgs &a, hipStream_t st) {
+    // pieces per record: the largest output slot bounds a literal (max_out 0: unknown, take 1 GiB)
+    const uint64_t mo = a.max_out ? a.max_out : (1ull << 30);
+    hipLaunchKernelGGL(kd_copy, dim3(2048), dim3(256), 0, st, a, (mo + 65535) / 65536);
+    return hipGetLastError();
+}
 
 hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t st) {
     const uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);

@@ -12,6 +12,11 @@ namespace ez {
 struct SpecState {
     uint32_t from, done, op, flags;
 };
+// K2w: a long literal kd_copy moves after the decoders (len bytes from in[src] to out[dst])
+struct DeferLit {
+    uint64_t src, dst, len;
+};
+constexpr int kDefSlots = 8;  // deferred literals per stream at most
 // a literal whose bytes K1x copies at the end (kx_copy): len bytes from in[src] to out[dst]
 struct SpecLit {
     uint64_t src, dst, len;
@@ -91,6 +96,8 @@ struct DecompressArgs {
     int64_t boff;             // handle: absolute offset of in[0]
     DecodeState *st;          // handle: state in/out
     uint32_t *slow;           // batch: [0] = count, [1..] = streams the fast path handed over (nullptr = exact path only)
+    uint32_t *defer;          // K2w: [0] = count, records (DeferLit) from word 4: long literals kd_copy moves
+    uint64_t defer_cap;       // records reserved
     uint64_t max_out;         // batch: host hint, largest output slot (0 = unknown)
     const uint32_t *todo;     // batch: [0] = count, [1..] = the streams to decode (nullptr = all)
 };
@@ -121,6 +128,7 @@ void select_decompress_variant(int v);
 // K2r: one lane per stream with a 512-byte LDS ring of recent output (ez_decompress_ring.hip)
 hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t s);
 hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t s);  // K2w, long streams
+hipError_t launch_defer_copy(const DecompressArgs &a, hipStream_t s);       // K2w's deferred literals
 bool lds_exchange_in_lane_order();  // the LDS property K1s-T32 relies on (checked once)
 hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
                        uint8_t *packed, uint64_t *packed_off, void *workspace, hipStream_t s);

@@ -147,3 +147,23 @@ def test_long_token_forms(cuda):
     """Len4 literals / copies, Off4 and OffLong+Off4 offsets, byte-checked on the device."""
     for name, b, ht, _ in long_form_inputs():
         _gpu_check(cuda, [b, b[:4096], b], htable=ht)
+
+
+@pytest.mark.gpu
+def test_k2w_deferred_literals(cuda):
+    """K2w defers literals of 16 KiB and more to a chip-wide copy (kd_copy) after giving its ring
+    their last 8 KiB: copies that read back into such a literal from beyond the ring (distances
+    16 KiB+), one to six long literals per stream (a stream defers up to 8; the rest are
+    moved inline), long literals right after short tokens and at the stream's end."""
+    rng = np.random.default_rng(61)
+    R = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in (20000, 17000, 40000, 16384, 70000, 30001)]
+    logs = __import__("eazy_amd.synth", fromlist=["logs"]).logs(63, 200000).tobytes()
+    bufs = [
+        R[0] + R[0][:3000] + R[0][100:700],                       # copies into the deferred literal
+        logs[:5000] + R[1] + logs[:5000] + R[1][5:900] + R[2],     # log tokens around two long literals
+        b"".join(R) + R[0][:64] + R[4][1000:1200] + R[5][7:99],    # six long literals, copies into several
+        R[3],                                                      # exactly 16 KiB, the whole stream
+        logs[:70000],                                              # no long literal
+        b"".join(R + R[:4]) + R[2][:500],                           # ten long literals: eight deferred
+    ]
+    _gpu_check(cuda, bufs)
