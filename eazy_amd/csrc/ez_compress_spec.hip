@@ -187,13 +187,28 @@ __global__ __launch_bounds__(1024) void kx_reset(CompressArgs A, KxBufs B) {
 // and candidate cand, take an action?  The general kernel's lane evaluation (ez_compress.hip,
 // "per-lane capped evaluation"), with 8-byte extensions: acceptance needs 6 bytes, and an
 // extension capped at 8 is accepted there before its exact length is known.
-__device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t *p, int64_t n, int64_t x, int64_t cand, int64_t done) {
+// 16 bytes at y from dword-aligned loads (a dwordx4 and a dword) + v_alignbyte: a byte-unaligned
+// 16-byte gather costs the L1 an access per dword it touches (tools/mb_ta.hip); near the batch's
+// edges the clamped path
+__device__ __forceinline__ V16 ld16_al(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
+    const uint8_t *a = (const uint8_t *)((uintptr_t)y & ~(uintptr_t)3);
+    if (a < lo || a + 20 > hi) return ld_clamped(y, lo, hi);
+    const uint32_t r = (uint32_t)((uintptr_t)y & 3);
+    const uint4 q = *(const uint4 *)a;
+    const uint32_t w4 = *(const uint32_t *)(a + 16);
+    const uint32_t e0 = __builtin_amdgcn_alignbyte(q.y, q.x, r), e1 = __builtin_amdgcn_alignbyte(q.z, q.y, r);
+    const uint32_t e2 = __builtin_amdgcn_alignbyte(q.w, q.z, r), e3 = __builtin_amdgcn_alignbyte(w4, q.w, r);
+    return V16{(uint64_t)e0 | ((uint64_t)e1 << 32), (uint64_t)e2 | ((uint64_t)e3 << 32)};
+}
+
+// vx = stream bytes x-8 .. x+7
+__device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t *p, int64_t n, int64_t x, int64_t cand, int64_t done,
+                                           const V16 vx) {
     const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
-    const V16 vx = ld_clamped(p + x - 8, lo, hi);  // stream bytes x-8 .. x+7
     const int64_t bs = A.bs;
     if (cand >= done && x > cand) {
         // off >= 0 and i > done + off: writeRunlen with st = cand (writer.go:227-231, 441-473)
-        const V16 vc = ld_clamped(p + cand - 8, lo, hi);
+        const V16 vc = ld16_al(p + cand - 8, lo, hi);
         if (cand + 8 < n && vc.hi == 0) return true;  // writeZeros: >= 8 zeros at st
         const uint64_t df = vx.hi ^ vc.hi, db = vx.lo ^ vc.lo;
         int64_t f = df ? (int64_t)(__builtin_ctzll(df) >> 3) : 8;
@@ -208,7 +223,7 @@ __device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t 
     // holds stream byte done - bs + ((y - done) & mask), zero before the stream
     V16 vc;
     if (cand - 8 >= 0 && cand - 8 >= done - bs && cand + 8 <= done) {
-        vc = ld16v(p + cand - 8);
+        vc = ld16_al(p + cand - 8, lo, hi);
     } else {
         vc = V16{0, 0};
         const int64_t mask = bs - 1;
@@ -236,27 +251,52 @@ __device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t 
 // early pieces of every active stream are judged first and a stream's later pieces are skipped
 // once an accepted position before them is known
 __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
+    __shared__ uint32_t S[kPiece / 4 + 8];  // the piece's bytes x-8 .. x+23 for its 256 positions, as aligned words
+    __shared__ bool skip;
     const uint64_t nact = B.nact[0];
     const uint64_t kp = (A.max_len + kPiece - 1) / kPiece + 1;
     const uint32_t hsh = hshift(A.hs);
     const int lane = (int)(threadIdx.x & 63);
+    const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
     for (uint64_t q = blockIdx.x; q < nact * kp; q += gridDim.x) {
         const uint64_t j = q / nact, s = B.act[q % nact];
         const SpecState sp = A.spec[s];
         const int64_t n = slen(A, s), from = sp.from, done = sp.done;
         const int64_t xb = (from & ~(kPiece - 1)) + (int64_t)j * kPiece;
-        if (xb + 4 > n || xb > (int64_t)__atomic_load_n(&B.first[s], __ATOMIC_RELAXED)) continue;
+        if (xb + 4 > n) continue;  // uniform: the block's values only
+        const uint8_t *p = A.in + A.in_off[s];
+        // stage bytes [xb - 8, xb + kPiece + 24) by coalesced aligned words (outside the batch: 0);
+        // whether an accept before the piece is known already is read once, by thread 0 (another
+        // block's atomicMin may land between two threads' reads: the decision must be the block's)
+        const uint8_t *wa = (const uint8_t *)((uintptr_t)(p + xb - 8) & ~(uintptr_t)3);
+        const uint32_t r0 = (uint32_t)((uintptr_t)(p + xb - 8) & 3);
+        __syncthreads();  // the previous piece's readers are done
+        if (threadIdx.x == 0) skip = xb > (int64_t)__atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
+        if (threadIdx.x < kPiece / 4 + 8) {
+            const uint8_t *w = wa + 4 * threadIdx.x;
+            uint32_t v = 0;
+            if (w >= lo && w + 4 <= hi) v = *(const uint32_t *)w;
+            else
+                for (int t = 0; t < 4; t++)
+                    if (w + t >= lo && w + t < hi) v |= (uint32_t)w[t] << (8 * t);
+            S[threadIdx.x] = v;
+        }
+        __syncthreads();
+        if (skip) continue;
         const int64_t x = xb + threadIdx.x;
         bool acc = false;
         if (x >= from && x + 4 <= n) {
-            const uint8_t *p = A.in + A.in_off[s];
-            const uint32_t h = hash4(p + x, hsh);
+            const uint32_t o = r0 + threadIdx.x, k = o >> 2, r = o & 3;
+            const uint32_t d0 = S[k], d1 = S[k + 1], d2 = S[k + 2], d3 = S[k + 3], d4 = S[k + 4];
+            const V16 vx{(uint64_t)__builtin_amdgcn_alignbyte(d1, d0, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32),
+                         (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, r) << 32)};
+            const uint32_t h = ((uint32_t)vx.hi * kHashMul) >> hsh;
             const uint16_t d = B.pred[A.in_off[s] - A.in_off[0] + x];
             // nearest earlier same-hash position (chunk-local, else the chunk's incoming entry);
             // before `from` the table at `from` holds the entry
             const int64_t pc = d ? x - d : (int64_t)B.tabs[(s * B.kmax + (uint64_t)(x / kChunk)) * (uint64_t)A.hs + h];
             const int64_t cand = pc >= from ? pc : (int64_t)A.spec_tab[s * (uint64_t)A.hs + h];
-            acc = kx_accepts(A, p, n, x, cand, done);
+            acc = kx_accepts(A, p, n, x, cand, done, vx);
         }
         const uint64_t m = wballot(acc);
         if (m && lane == ffs64(m)) atomicMin(&B.first[s], (uint32_t)x);
