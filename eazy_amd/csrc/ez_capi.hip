@@ -611,10 +611,13 @@ static int compress_batch_impl(int64_t block, int64_t htable, int flags, const e
     if (write_idx && b->count == 0) return EZ_OK;
     const bool split_mw = write_idx && ez::split_stride_words(a) != 0;
     const uint64_t words = split_mw ? ez::split_scratch_words(a) : ez::compress_scratch_words(a);
+    // the scratch of this (device, stream) stays locked through the launches: another host thread
+    // growing it meanwhile would free what these kernels were given
+    std::unique_lock<std::mutex> lk(g_mu, std::defer_lock);
     if (words) {
         int dev = 0;
         EZ_HIP(hipGetDevice(&dev));
-        std::lock_guard<std::mutex> lk(g_mu);
+        lk.lock();
         Scratch &sc = g_scratch[std::make_pair(dev, hip_stream)];
         if (sc.ht.ensure((size_t)words * 4)) return EZ_EDEVICE;
         a.ht_global = sc.ht.as<uint32_t>();
