@@ -200,9 +200,8 @@ struct PredZ<0> {
 };
 
 // ---------------------------------------------------------------- K1p
-// GIN: stream bytes read through L1/L2 (GW); else staged in LDS after the table (PW)
 // MW: streams of several Writes (CompressArgs::write_idx), else one Write each
-template <int G, bool T16, bool GIN, bool MW>
+template <int G, bool T16, bool MW>
 __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                   uint64_t rcap, int prio) {
     constexpr int S = 64 / G;
@@ -223,34 +222,10 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
         gp = A.in + A.in_off[s];
     }
-    using SRC = typename std::conditional<GIN, GW, PW>::type;
-    SRC P;
-    if constexpr (GIN) {
-        P.p = gp;
-        P.blo = A.in;
-        P.bhi = A.in + A.in_off[A.count];
-    } else {  // [4 zero words][the stream's words][zero words to the stride's end]
-        uint32_t *pw = htw + table_words;
-        const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
-        const uint32_t r = (uint32_t)((uintptr_t)gp & 3);
-        const int32_t nw = have ? (int32_t)((r + (uint32_t)n + 3) >> 2) : 0;
-        const uint8_t *gb = gp - r;
-        P.w = pw;
-        P.pb = 16 + r;
-        for (int32_t k = lj; k < (int32_t)(stride_words - table_words); k += G) {
-            uint32_t v = 0;
-            const int32_t wk = k - 4;
-            if (wk >= 0 && wk < nw) {
-                const uint8_t *q = gb + 4 * wk;
-                if (q >= lo && q + 4 <= hi) v = *(const uint32_t *)q;
-                else
-                    for (int t = 0; t < 4; t++) v |= (q + t >= lo && q + t < hi) ? (uint32_t)q[t] << (8 * t) : 0u;
-                if (wk == 0) v &= ~0u << (8 * r);
-                v = low_bytes32(v, n - (4 * wk - (int32_t)r));
-            }
-            pw[k] = v;
-        }
-    }
+    GW P;  // stream bytes through L1/L2 (staging them in LDS after the table cost residency: round 1)
+    P.p = gp;
+    P.blo = A.in;
+    P.bhi = A.in + A.in_off[A.count];
     uint64_t *rec = recs + (have ? s * rcap : 0);
     // ht zero = stream position 0 (writer.go:183, A.2)
     for (int32_t k = 4 * lj; k < (int32_t)table_words; k += 4 * G) *(uint4 *)(htw + k) = make_uint4(0, 0, 0, 0);
@@ -375,7 +350,7 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
         EZ_PROF_MARK(2);
         const int32_t blim = zr ? ca - done : (rl ? ((xa - done) < ca - wstart ? (xa - done) : ca - wstart) : xa - done);
         int32_t fx, cx;
-        gext<G, SRC>(P, act && fk == 24, act && bk8 == 8, g, lj, fa, ca, mode, done, 24, wend - fa, blim, fx, cx);
+        gext<G, GW>(P, act && fk == 24, act && bk8 == 8, g, lj, fa, ca, mode, done, 24, wend - fa, blim, fx, cx);
         const int32_t f = fk == 24 ? fx : fk;
         const int32_t c = bk8 == 8 ? cx : bk8;
         EZ_PROF_MARK(3);
@@ -927,8 +902,7 @@ __global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint64_t *r
     }
 }
 
-// LDS words of a stream's table, and of its staged input (GIN false: 4 zero
-// words, the stream, 8 zero words; 0 = this variant cannot take the batch)
+// LDS words of a stream's table (0 = this variant cannot take the batch)
 template <bool T16>
 uint32_t split_table_words(const CompressArgs &a) {
     if (a.ring || a.max_len == 0 || 2 * (int64_t)a.max_len > a.bs || a.hs > 4096 || a.hs < 4) return 0;
@@ -936,11 +910,11 @@ uint32_t split_table_words(const CompressArgs &a) {
     const uint64_t words = T16 ? ((uint64_t)a.hs + 1) / 2 : (uint64_t)a.hs;
     return (uint32_t)((words + 3) & ~3ull);
 }
-template <int G, bool T16, bool GIN>
+template <int G, bool T16>
 uint32_t split_stride(const CompressArgs &a) {
     const uint64_t tw = split_table_words<T16>(a);
     if (tw == 0) return 0;
-    const uint64_t w = tw + (GIN ? 0 : ((4 + (a.max_len + 3) / 4 + 8 + 3) & ~3ull));
+    const uint64_t w = tw;
     if (w * 4 * (64 / G) > 160 * 1024) return 0;
     return (uint32_t)w;
 }
@@ -958,15 +932,15 @@ bool split_t32_forced() {
     return v || g_split_t32;
 }
 
-template <int G, bool T16, bool GIN, bool MW>
+template <int G, bool T16, bool MW>
 hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_parse<G, T16, GIN, MW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_parse<G, T16, MW>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
     constexpr int S = 64 / G;
-    const uint32_t stride = split_stride<G, T16, GIN>(a), tw = split_table_words<T16>(a);
+    const uint32_t stride = split_stride<G, T16>(a), tw = split_table_words<T16>(a);
     const uint64_t rcap = rec_cap(a);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
@@ -975,7 +949,7 @@ hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st)
     // bit 1 around the next window's load; EZ_K1S_PRIO=0|1|2|3 (A/B, same box: 3.58 / 3.52 /
     // 3.58 / 3.53 ms at C1)
     static const int prio = getenv("EZ_K1S_PRIO") ? atoi(getenv("EZ_K1S_PRIO")) : 1;
-    hipLaunchKernelGGL((k1_parse<G, T16, GIN, MW>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap,
+    hipLaunchKernelGGL((k1_parse<G, T16, MW>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap,
                        prio);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -996,7 +970,7 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
         attr_done = true;
     }
     constexpr int S = 4;
-    const uint32_t stride = split_stride<16, true, true>(a), tw = split_table_words<true>(a);
+    const uint32_t stride = split_stride<16, true>(a), tw = split_table_words<true>(a);
     const uint64_t rcap = rec_cap(a);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     static const int prio = getenv("EZ_K1S_PRIO") ? atoi(getenv("EZ_K1S_PRIO")) : 1;
@@ -1074,8 +1048,8 @@ bool lds_store_in_lane_order() {
 // the table the batch takes: 16 (T16), 32 (T32) or 0 (K1s cannot take it)
 static int split_table(const CompressArgs &a) {
     if (a.count > (1ull << 31)) return 0;
-    if (!split_t32_forced() && split_stride<16, true, true>(a) != 0 && lds_store_in_lane_order()) return 16;
-    if (split_stride<16, false, true>(a) != 0 && lds_exchange_in_lane_order()) return 32;
+    if (!split_t32_forced() && split_stride<16, true>(a) != 0 && lds_store_in_lane_order()) return 16;
+    if (split_stride<16, false>(a) != 0 && lds_exchange_in_lane_order()) return 32;
     return 0;
 }
 
@@ -1093,13 +1067,13 @@ hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipSt
     uint64_t *recs = (uint64_t *)scratch;
     const int T = split_table(a);
     if (a.write_idx) {
-        if (T == 16) return launch_split_g<16, true, true, true>(a, recs, st);
-        if (split_g32(a.count) == 32) return launch_split_g<32, false, true, true>(a, recs, st);
-        return launch_split_g<16, false, true, true>(a, recs, st);
+        if (T == 16) return launch_split_g<16, true, true>(a, recs, st);
+        if (split_g32(a.count) == 32) return launch_split_g<32, false, true>(a, recs, st);
+        return launch_split_g<16, false, true>(a, recs, st);
     }
-    if (T == 16) return split_lean() ? launch_lean(a, recs, st) : launch_split_g<16, true, true, false>(a, recs, st);
-    if (split_g32(a.count) == 32) return launch_split_g<32, false, true, false>(a, recs, st);
-    return launch_split_g<16, false, true, false>(a, recs, st);
+    if (T == 16) return split_lean() ? launch_lean(a, recs, st) : launch_split_g<16, true, false>(a, recs, st);
+    if (split_g32(a.count) == 32) return launch_split_g<32, false, false>(a, recs, st);
+    return launch_split_g<16, false, false>(a, recs, st);
 }
 
 }  // namespace ez

@@ -28,7 +28,7 @@ constexpr int32_t kWR = 8192;      // output ring bytes per stream (power of two
 constexpr int32_t kWIn = 1024;     // input ring bytes per stream (power of two)
 constexpr int32_t kWStage = 512;   // input staged this many bytes at a time (32 lanes x 16)
 constexpr int32_t kWChunk = 1024;  // output leaves the ring this many bytes at a time
-constexpr size_t kWLds = 16 + (size_t)kWR + 32 + kWIn + 16;
+constexpr size_t kWLds = 16 + (size_t)kWR + 32 + kWIn + 16 + 12 * kDefSlots;  // rings, deferred literals
 // Long literals (C4: a whole fp32 bucket is one literal) are not moved through the ring by the
 // stream's one wave (1 KiB per pass, one HBM round trip each): their tag is parsed, the ring gets
 // their last 8 KiB, and kd_copy moves their bytes with the whole chip afterwards.  A far copy
@@ -79,30 +79,30 @@ __device__ __forceinline__ V16 ld_in(const uint8_t *y, const uint8_t *lo, const 
     return y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
 }
 
-// the 16 output bytes at sq (< the ring's reach) from HBM, or from the input where they lie in a
-// deferred literal (dd/ds/dl: its output position, input position, length; nd of them)
-__device__ __forceinline__ V16 far16(const uint8_t *out, int32_t cap, const uint8_t *b, int32_t sq, int nd, const int32_t *dd,
-                                     const int32_t *ds, const int32_t *dl) {
-    bool hit = false;
-#pragma unroll
-    for (int k = 0; k < kDefSlots; k++)
-        if (k < nd && sq < dd[k] + dl[k] && sq + 16 > dd[k]) hit = true;
-    if (!hit) return sq >= 0 ? ld16v(out + sq) : ld_clamped(out + sq, out, out + cap);
+// the 16 output bytes at sq (< the ring's reach) from HBM, or from the input where they lie in one
+// of the nd deferred literals (defs: {output position, input position, length} each, in LDS)
+__device__ __forceinline__ V16 far16_def(const uint8_t *out, int32_t cap, const uint8_t *b, int32_t sq, int nd, const int32_t *defs) {
     V16 v{0, 0};
     for (int t = 0; t < 16; t++) {
         const int32_t y = sq + t;
         uint64_t c = y >= 0 ? out[y] : 0;
-#pragma unroll
-        for (int k = 0; k < kDefSlots; k++)
-            if (k < nd && y >= dd[k] && y < dd[k] + dl[k]) c = b[ds[k] + (y - dd[k])];
+        for (int k = 0; k < nd; k++)
+            if (y >= defs[3 * k] && y < defs[3 * k] + defs[3 * k + 2]) c = b[defs[3 * k + 1] + (y - defs[3 * k])];
         if (t < 8) v.lo |= c << (8 * t);
         else v.hi |= c << (8 * (t - 8));
     }
     return v;
 }
+__device__ __forceinline__ V16 far16(const uint8_t *out, int32_t cap, const uint8_t *b, int32_t sq, int nd, const int32_t *defs) {
+    bool hit = false;
+    for (int k = 0; k < nd; k++)
+        if (sq < defs[3 * k] + defs[3 * k + 2] && sq + 16 > defs[3 * k]) hit = true;
+    if (!hit) return sq >= 0 ? ld16v(out + sq) : ld_clamped(out + sq, out, out + cap);
+    return far16_def(out, cap, b, sq, nd, defs);
+}
 
 // stream s by the whole wave; false = hand it over
-__device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring, uint8_t *inb, const int lane) {
+__device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring, uint8_t *inb, int32_t *defs, const int lane) {
     const uint8_t *b = A.in + A.in_off[s];
     const int64_t nb64 = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
     const uint8_t *in_end = A.in + A.in_off[A.count];
@@ -135,10 +135,7 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
     V16 pend = get_in(in_hi);
 
     int32_t i = 0, pos = 0, bsl = -1, fl = 0;  // fl: output below it is in HBM (or deferred)
-    int nd = 0;                                 // deferred literals of this stream
-    int32_t dd[kDefSlots], ds[kDefSlots], dl[kDefSlots];
-#pragma unroll
-    for (int k = 0; k < kDefSlots; k++) dd[k] = ds[k] = dl[k] = 0;
+    int nd = 0;                                 // deferred literals of this stream (defs: theirs, in LDS)
     // A group: tokens whose sources lie before the group's first output byte gpos
     // (literals staged in the input ring, copies with D >= L from the output ring),
     // cut into pieces of <= 16 bytes, one per lane: one LDS read and one exact write
@@ -291,9 +288,11 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
                     const uint32_t at = atomicAdd(&A.defer[0], 1u);
                     if (at < A.defer_cap) ((DeferLit *)(A.defer + 4))[at] = DeferLit{A.in_off[s] + (uint64_t)src, A.out_off[s] + (uint64_t)pos, (uint64_t)L};
                 }
-#pragma unroll
-                for (int k = 0; k < kDefSlots; k++)
-                    if (k == nd) { dd[k] = pos; ds[k] = src; dl[k] = L; }
+                if (lane == 0) {
+                    defs[3 * nd] = pos;
+                    defs[3 * nd + 1] = src;
+                    defs[3 * nd + 2] = L;
+                }
                 nd++;
                 pos += L;
                 fl = pos;
@@ -324,7 +323,7 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
                     if (act) {
                         V16 v = pv;
                         if (!t.cp) v = staged ? rld<kWIn>(inb, src + q) : ld_in(b + src + q, A.in, in_end);
-                        else if (D >= 16) v = sq >= rlo ? rld<kWR>(ring, sq) : far16(out, cap, b, sq, nd, dd, ds, dl);
+                        else if (D >= 16) v = sq >= rlo ? rld<kWR>(ring, sq) : far16(out, cap, b, sq, nd, defs);
                         rst<kWR>(ring, pos + q, v);
                     }
                     const int32_t fin = pos + (done + W < L ? done + W : L);  // final bytes end here
@@ -356,9 +355,10 @@ __device__ bool wave_one(const DecompressArgs &A, const uint64_t s, uint8_t *rin
 __global__ __launch_bounds__(64) void k2_wave(DecompressArgs A) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     uint8_t *ring = smem + 16, *inb = smem + 16 + kWR + 32;
+    int32_t *defs = (int32_t *)(smem + 16 + kWR + 32 + kWIn + 16);
     const int lane = (int)threadIdx.x;
     for (uint64_t s = blockIdx.x; s < A.count; s += gridDim.x)
-        if (!wave_one(A, s, ring, inb, lane) && lane == 0) {
+        if (!wave_one(A, s, ring, inb, defs, lane) && lane == 0) {
             const uint32_t at = atomicAdd(&A.slow[0], 1u);
             A.slow[1 + at] = (uint32_t)s;
         }

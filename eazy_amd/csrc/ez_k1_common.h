@@ -1,5 +1,5 @@
 // ez_k1_common.h — pieces of the group-per-stream K1 kernels (ez_compress_split.hip):
-// byte views of a stream (staged in LDS, or read through L1/L2), group
+// the byte view of a stream read through L1/L2, group
 // ballots/broadcasts, the branch-free Encoder.Tag / Encoder.Offset
 // (writer.go:537-597) and the cooperative exact match count.
 #pragma once
@@ -16,22 +16,6 @@ __device__ __forceinline__ uint32_t gball(bool p, int g) {
     return (uint32_t)(((uint64_t)__ballot(p) >> (G * g)) & (G == 32 ? 0xffffffffull : ((1ull << G) - 1)));
 }
 __device__ __forceinline__ int32_t bcast(int32_t v, int src_lane) { return __shfl(v, src_lane, 64); }
-
-// byte view of a stream staged in LDS: word array w, byte 0 of the stream at byte pb of w
-struct PW {
-    const uint32_t *w;
-    uint32_t pb;
-    __device__ __forceinline__ uint32_t b(int32_t y) const { return ((const uint8_t *)w)[pb + y]; }
-    __device__ __forceinline__ uint32_t u32(int32_t y) const { return words_u32(w, (uint32_t)(pb + y)); }
-    // 8 bytes before y and 8 bytes from y (the staging pads make y-8 .. y+8 readable)
-    __device__ __forceinline__ void around(int32_t y, uint64_t &before, uint64_t &from) const {
-        const uint32_t a = pb + y - 8;
-        const uint32_t k = a >> 2, sh = a & 3;
-        const uint32_t w0 = w[k], w1 = w[k + 1], w2 = w[k + 2], w3 = w[k + 3], w4 = w[k + 4];
-        before = (uint64_t)__builtin_amdgcn_alignbyte(w1, w0, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w2, w1, sh) << 32);
-        from = (uint64_t)__builtin_amdgcn_alignbyte(w3, w2, sh) | ((uint64_t)__builtin_amdgcn_alignbyte(w4, w3, sh) << 32);
-    }
-};
 
 // byte view of a stream read straight from HBM (through L1/L2): p = the
 // stream's first byte, [blo, bhi) = the batch (>= 16 bytes), loads never leave
