@@ -143,7 +143,8 @@ def compress_kernel(block: int, htable: int, max_len: int, count: int) -> str:
 
 def select_compress_kernel(kind: str = "") -> None:
     """Force the K1 kernel of later batch calls ('s' K1s, 'S' K1s with the u32
-    exchange table, 'w' general alone, 'x' K1x's rounds for any fresh single-Write batch;
+    exchange table, 'w' general alone, 'x' K1x's rounds for any fresh single-Write batch,
+    'l' K1L (the lean parse with the window's ring semantics) alone;
     '' = automatic).  Tests and A/B measurement only."""
     _check(_lib().ez_select_compress_kernel(ord(kind) if kind else 0))
 

@@ -660,7 +660,7 @@ extern "C" int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_le
 }
 
 extern "C" int ez_select_compress_kernel(int kind) {
-    if (kind != 0 && !strchr("sSwx", kind)) return EZ_EINVAL;
+    if (kind != 0 && !strchr("sSwxl", kind)) return EZ_EINVAL;
     ez::select_split_table(kind == 'S');
     ez::select_compress_variant(kind == 'S' ? 's' : kind);
     return EZ_OK;

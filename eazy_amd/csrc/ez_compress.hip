@@ -695,6 +695,7 @@ uint64_t compress_scratch_words(const CompressArgs &a) {
     const char v = compress_variant(a);
     if (v == 's') return split_scratch_words(a);
     if (v == 'x') return (spec_scratch_bytes(a) + 3) / 4;
+    if (v == 'l') return (long_scratch_bytes(a) + 3) / 4;
     if (a.hs <= kHtLdsMax) return 0;
     const uint64_t grid = a.count < 2048 ? a.count : 2048;
     return grid * (uint64_t)a.hs;
@@ -717,6 +718,7 @@ char compress_variant(const CompressArgs &a) {
         forced = e && std::string(e) == "general" ? 'w' : 0;
     }
     if (forced == 'w') return 'w';
+    if (forced == 'l' && long_applies(a)) return 'l';  // K1L alone (tests, A/B)
     if (split_stride_words(a) != 0 && forced != 'x') return 's';
     return spec_applies(a, forced == 'x') ? 'x' : 'w';
 }
@@ -727,6 +729,7 @@ hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     if (v == 's') return launch_compress_split(a, a.ht_global, st);
     // long fresh streams: K1x rounds, which call the general kernel to resolve emitting positions
     if (v == 'x') return launch_compress_spec(a, (uint8_t *)a.ht_global, st);
+    if (v == 'l') return launch_long(a, (uint8_t *)a.ht_global, st);
     return launch_general(a, st);
 }
 

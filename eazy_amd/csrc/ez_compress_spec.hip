@@ -360,7 +360,7 @@ int rounds() {
 }
 
 struct Layout {
-    uint64_t pred, tabs, first, spec, spec_tab, act, nact, lit, total, lit_cap;
+    uint64_t pred, tabs, first, spec, spec_tab, act, nact, lit, lrec, total, lit_cap;
 };
 
 Layout layout(const CompressArgs &a) {
@@ -376,7 +376,8 @@ Layout layout(const CompressArgs &a) {
     l.act = l.spec_tab + up(a.count * (uint64_t)a.hs * 4);
     l.nact = l.act + up(a.count * 4);
     l.lit = l.nact + 256;
-    l.total = l.lit + up(l.lit_cap * sizeof(SpecLit));
+    l.lrec = l.lit + up(l.lit_cap * sizeof(SpecLit));
+    l.total = l.lrec + (long_applies(a) ? up(long_scratch_bytes(a)) : 0);  // K1L's records
     return l;
 }
 
@@ -435,11 +436,14 @@ hipError_t launch_compress_spec(const CompressArgs &a0, uint8_t *scratch, hipStr
         a.spec_mode = 1;
         if ((e = launch_general(a, st)) != hipSuccess) return e;
     }
-    // the streams still active: the general kernel from where they stand; then every literal's bytes
+    // the streams still active (dense accepts, C4s): K1L from where they stand (the general kernel
+    // where K1L cannot take the batch); then every recorded literal's bytes
     hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B);
     if (!check()) return e;
     a.spec_mode = 2;
-    if ((e = launch_general(a, st)) != hipSuccess) return e;
+    if (long_applies(a0)) e = launch_long(a, scratch + l.lrec, st);
+    else e = launch_general(a, st);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kx_copy, dim3(jgrid), dim3(256), 0, st, a, B);
     if (!check()) return e;
     if (getenv("EZ_K1X_DEBUG")) {  // diagnostics: streams left to the general kernel's serial continuation

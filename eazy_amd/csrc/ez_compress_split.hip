@@ -709,6 +709,284 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
     nrec_out = nrec;
 }
 
+// ---------------------------------------------------------------- K1L: long fresh streams
+// k1_lean's parse for Writes longer than half the block (C4's gradient buckets, where K1x's rounds
+// leave dense streams such as C4s to it): the same window, DPP predecessor search and capped
+// judgement, plus the window's ring semantics of writer.go -- far skip (:219-221), the cut branch of
+// writeRunlen (:464-473), trim 1 (:280-286) and the ring image before the window, block[y & mask] =
+// stream byte y + bs for y < w.pos - bs -- a u32 table, bounds-checked loads (any
+// stream of a batch, no edge slots), and 16-byte records.  It resumes the streams K1x hands over
+// (spec state: position, pending literal, output so far, table).
+struct WideRec {
+    uint32_t lit_end, clen, dist, flags;  // flags bit 0: force the literal (writeRunlen, A.6)
+};
+
+// a dword at w, 0 for bytes outside the batch [lo, hi)
+__device__ __forceinline__ uint32_t dw_chk(const uint8_t *w, const uint8_t *lo, const uint8_t *hi) {
+    if (w >= lo && w + 4 <= hi) return *(const uint32_t *)w;
+    uint32_t v = 0;
+    for (int t = 0; t < 4; t++)
+        if (w + t >= lo && w + t < hi) v |= (uint32_t)w[t] << (8 * t);
+    return v;
+}
+struct WinDwL : WinDw {
+    __device__ __forceinline__ void load(const uint8_t *p, int32_t i, int lj, const uint8_t *lo, const uint8_t *hi) {
+        const uintptr_t a = (uintptr_t)(p + i - 8);
+        r0 = (uint32_t)(a & 3);
+        dw = dw_chk((const uint8_t *)((a & ~(uintptr_t)3) + 4 * (uint32_t)lj), lo, hi);
+    }
+};
+// bytes y-8 .. y+23 (bytes outside the batch read 0)
+__device__ __forceinline__ void bytes32_chk(const uint8_t *p, int32_t y, V16 &c0, V16 &c1, const uint8_t *lo, const uint8_t *hi) {
+    const uintptr_t a = (uintptr_t)(p + y - 8);
+    const uint8_t *w = (const uint8_t *)(a & ~(uintptr_t)3);
+    if (w >= lo && w + 36 <= hi) {
+        bytes32(LeanIn{}, p, y, c0, c1);
+        return;
+    }
+    const uint32_t r = (uint32_t)(a & 3);
+    uint32_t d[9];
+    for (int t = 0; t < 9; t++) d[t] = dw_chk(w + 4 * t, lo, hi);
+    uint32_t b[8];
+    for (int t = 0; t < 8; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+    c0 = V16{(uint64_t)b[0] | ((uint64_t)b[1] << 32), (uint64_t)b[2] | ((uint64_t)b[3] << 32)};
+    c1 = V16{(uint64_t)b[4] | ((uint64_t)b[5] << 32), (uint64_t)b[6] | ((uint64_t)b[7] << 32)};
+}
+// 16 bytes from y of the window's ring image at w.pos = done (bytes y >= done: 0, capped away by
+// trim 2; y < done - bs: stream byte y + bs; before the stream: 0)
+__device__ __forceinline__ V16 ring16(const GW &P, int32_t y, int32_t done, int64_t bs) {
+    uint64_t lo, hi;
+    P.around(y + 8, lo, hi);
+    V16 v = keep_low16(V16{lo, hi}, done - y);
+    const int64_t edge = (int64_t)done - bs;
+    if ((int64_t)y < edge) {
+        P.around((int32_t)((int64_t)y + bs + 8), lo, hi);
+        const int32_t k = (int32_t)(edge - y);  // bytes 0 .. k-1 lie before the window
+        const V16 m = keep_low16(V16{~0ull, ~0ull}, k);
+        v = V16{(v.lo & ~m.lo) | (lo & m.lo), (v.hi & ~m.hi) | (hi & m.hi)};
+    }
+    return v;
+}
+// gext with the long window's ring image on the source side (mode 2: ring16; 0 zeros; 1 stream)
+template <int G>
+__device__ __forceinline__ void gext_long(const GW &P, bool runf, bool runb, int g, int lj, int32_t a, int32_t b, int mode,
+                                          int32_t done, int64_t bs, int32_t fromf, int32_t limf, int32_t limb, int32_t &resf,
+                                          int32_t &resb) {
+    constexpr int H = G / 2;
+    constexpr uint32_t kHalf = (1u << H) - 1;
+    const bool fw = lj < H;
+    const int t = lj % H;
+    resf = fromf < limf ? fromf : limf;
+    resb = 8 < limb ? 8 : limb;
+    bool gof = runf && fromf < limf, gob = runb && 8 < limb;
+    int32_t basef = fromf, baseb = 8;
+    while (__ballot(gof || gob) != 0) {
+        const bool mine = fw ? gof : gob;
+        const int32_t lim = fw ? limf : limb;
+        const int32_t k = (fw ? basef : baseb) + 16 * t;
+        int32_t mb = 16;
+        if (mine) {
+            if (k < lim) {
+                const int32_t ya = fw ? a + k : a - k - 16, yb = fw ? b + k : b - k - 16;
+                uint64_t alo, ahi;
+                P.around(ya + 8, alo, ahi);
+                V16 vb{0, 0};
+                if (mode == 1) P.around(yb + 8, vb.lo, vb.hi);
+                else if (mode == 2) vb = ring16(P, yb, done, bs);
+                const uint64_t dl = alo ^ vb.lo, dh = ahi ^ vb.hi;
+                if (fw) mb = dl ? (int32_t)(__builtin_ctzll(dl) >> 3) : (dh ? 8 + (int32_t)(__builtin_ctzll(dh) >> 3) : 16);
+                else mb = dh ? (int32_t)(__builtin_clzll(dh) >> 3) : (dl ? 8 + (int32_t)(__builtin_clzll(dl) >> 3) : 16);
+                if (mb > lim - k) mb = lim - k;
+            } else {
+                mb = 0;
+            }
+        }
+        const uint32_t bad = gball<G>(mine && mb < 16, g);
+        const uint32_t bf = bad & kHalf, bb = bad >> H;
+        const int lf = bf ? __builtin_ctz(bf) : 0, lb = bb ? __builtin_ctz(bb) : 0;
+        const int32_t mbf = bcast(mb, G * g + lf), mbb = bcast(mb, G * g + H + lb);
+        if (gof) {
+            if (bf) {
+                resf = basef + 16 * lf + mbf;
+                resf = resf < limf ? resf : limf;
+                gof = false;
+            } else {
+                basef += 16 * H;
+                if (basef >= limf) { resf = limf; gof = false; }
+            }
+        }
+        if (gob) {
+            if (bb) {
+                resb = baseb + 16 * lb + mbb;
+                resb = resb < limb ? resb : limb;
+                gob = false;
+            } else {
+                baseb += 16 * H;
+                if (baseb >= limb) { resb = limb; gob = false; }
+            }
+        }
+    }
+}
+
+// the parse of one stream by a 16-lane group from (i, done) with the table in htw
+__device__ __forceinline__ void long_loop(const uint8_t *p, int32_t n, int32_t i, int32_t done, int64_t bs, int lj, int g,
+                                          uint32_t *htw, uint32_t hsh, uint4 *rec, uint64_t rcap, const uint8_t *blo,
+                                          const uint8_t *bhi, int32_t &nrec_out, int &err) {
+    constexpr int G = 16;
+    int32_t nrec = 0;
+    bool live = !err && i + 4 <= n;
+    int64_t guard = 4 * (int64_t)n + 64;
+    V16 w0{0, 0}, w1{0, 0};  // bytes x-8 .. x+7 and x+8 .. x+23 of this lane's position x
+    WinDwL wd;
+    wd.dw = 0;
+    wd.r0 = 0;
+    const GW P{p, blo, bhi};
+    wd.load(p, live ? i : 0, lj, blo, bhi);
+    while (__ballot(live) != 0) {
+        wd.bytes(g, lj, w0, w1);
+        if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
+        const int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
+        const int32_t x = i + lj;
+        const bool valid = live && lj < nvalid;
+
+        // ---- visit (writer.go:213-217): hash, table, nearest earlier lane with the same hash
+        const uint32_t h = valid ? ((uint32_t)w0.hi * kHashMul) >> hsh : 0u;
+        const int32_t tv = valid ? (int32_t)htw[h] : 0;
+        const int32_t d = PredZ<G - 1>::get(valid ? h + 1 : 0u, 0);
+        const int32_t cand = valid ? (d ? x - d : tv) : 0;
+        const bool rl = cand >= done && cand < x;
+        const bool far = !rl && (int64_t)done - cand > bs;  // writer.go:221-224
+        V16 c0{0, 0}, c1{0, 0};
+        if (valid && !far) {
+            bytes32_chk(p, cand, c0, c1, blo, bhi);
+            c0.lo &= cand >= 8 ? ~0ull : (cand <= 0 ? 0ull : ~0ull << (8 * (8 - cand)));  // before the stream: the fresh ring's zeros
+            if (!rl && (int64_t)cand - 8 < (int64_t)done - bs) c0.lo = ring16(P, cand - 8, done, bs).lo;  // rare
+        }
+
+        // ---- capped judgement, writer.go:219-301 (window) and :441-473 (writeRunlen, cut)
+        const uint64_t e0 = w0.hi ^ c0.hi, e1 = w1.lo ^ c1.lo, e2 = w1.hi ^ c1.hi;
+        int32_t jf = first_diff24(e0, e1, e2);
+        jf = jf < n - x ? jf : n - x;
+        int32_t bl = x - done;
+        if (rl) bl = bl < cand ? bl : cand;
+        int32_t jb = last_diff8(w0.lo ^ c0.lo);
+        jb = jb < bl ? jb : bl;
+        const bool zr = rl && c0.hi == 0 && cand + 8 < n;
+        const int32_t fw = rl ? jf : (jf < done - cand ? jf : done - cand);
+        const int64_t t1 = bs - (int64_t)(x - cand);  // trim 1: the copy ends within bs of x
+        const int32_t len = rl ? fw + jb : (int32_t)((int64_t)(fw + jb) < t1 ? (int64_t)(fw + jb) : (t1 < 0 ? -1 : t1));
+        const bool acc = valid && !far && (zr || len >= kMinCopyChunk);
+        const bool cut = rl && !zr && (int64_t)(x - cand) >= bs - 8;
+
+        // ---- this lane's action if it is the group's first acceptor
+        int32_t lit, nx, dist, ext;
+        bool force = false;
+        if (zr) {  // writeZeros :407-439
+            int32_t zf = first_diff24(0, c1.lo, c1.hi);
+            zf = zf < n - cand ? zf : n - cand;
+            int32_t zb = last_diff8(c0.lo);
+            zb = zb < cand - done ? zb : cand - done;
+            lit = cand - zb;
+            nx = cand + zf;
+            dist = 0;
+            ext = (zf == 24 && n - cand > 24 ? 1 : 0) | (zb == 8 && cand - done > 8 ? 2 : 0);
+        } else if (cut) {  // the cut branch: a literal to done + i - st, no copy (writer.go:464-473)
+            lit = done + (x - cand);
+            nx = lit;
+            dist = 0;
+            ext = 0;
+        } else {  // writeRunlen :441-489 / window match :303-321
+            lit = x - jb;
+            nx = lit + len;
+            dist = x - cand;
+            force = rl;
+            const int32_t room = rl ? n - x : (done - cand < n - x ? done - cand : n - x);
+            ext = (jf == 24 && room > 24 && (rl || (int64_t)(jb + 24) < t1) ? 1 : 0) | (jb == 8 && bl > 8 ? 2 : 0);
+        }
+        const uint64_t am64 = __ballot(acc);
+        const uint32_t am = (uint32_t)(am64 >> (G * g)) & 0xffffu;
+        const int a = am ? __builtin_ctz(am) : -1;
+        const bool act = live && a >= 0;
+        const int al = G * g + (a < 0 ? 0 : a);
+        int32_t nxt = bcast(nx, al);
+        const int32_t ea = bcast(ext, al);
+        if (__ballot(act && ea != 0) != 0) {
+            // rare: a saturated count; exact lengths by the whole group
+            const int32_t xa = i + (a < 0 ? 0 : a);
+            const int32_t ca = bcast(cand, al), jba = bcast(jb, al), fwa = bcast(zr ? nx - cand : fw, al);
+            const int32_t fl = bcast((int32_t)rl | ((int32_t)zr << 1), al);
+            const bool rla = fl & 1, zra = (fl >> 1) & 1;
+            const bool need = act && ea != 0;
+            const int mode = zra ? 0 : (rla ? 1 : 2);
+            const int32_t fa = zra ? ca : xa;
+            const int32_t blim = zra ? ca - done : (rla ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
+            const int32_t flim = zra ? n - ca : (rla ? n - xa : ((done - ca) < n - xa ? done - ca : n - xa));
+            int32_t fx, cx;
+            gext_long<G>(P, need && (ea & 1), need && (ea & 2), g, lj, fa, ca, mode, done, bs, 24, flim, blim, fx, cx);
+            if (need) {
+                int32_t f = (ea & 1) ? fx : fwa;
+                const int32_t c = (ea & 2) ? cx : (zra ? fa - bcast(lit, al) : jba);
+                if (!zra && !rla) {  // trim 1 on the exact lengths
+                    const int64_t t1a = bs - (int64_t)(xa - ca);
+                    if ((int64_t)(f + c) > t1a) f = (int32_t)(t1a - c);
+                }
+                nxt = fa + f;
+                if (lj == a) {
+                    lit = fa - c;
+                    nx = nxt;
+                }
+            }
+        }
+        // ---- table: the visited lanes' positions (the last of a hash wins), then lane a's i+1
+        if (valid && (a < 0 || lj <= a)) htw[h] = (uint32_t)x;
+        if (act && lj == a) {
+            if (!rl && !zr && x + 1 + 4 <= n) htw[((uint32_t)(w0.hi >> 8) * kHashMul) >> hsh] = (uint32_t)(x + 1);
+            if ((uint64_t)nrec < rcap)
+                __builtin_nontemporal_store(u32x4{(uint32_t)lit, (uint32_t)(nx - lit), (uint32_t)dist, force ? 1u : 0u}, (u32x4 *)(rec + nrec));
+        }
+        if (act) {
+            if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
+            nrec++;
+            i = done = nxt;
+        } else if (live) {
+            i += nvalid;
+        }
+        if (live && (err || i + 4 > n)) live = false;
+        wd.load(p, live ? i : 0, lj, blo, bhi);  // the next window's bytes
+    }
+    nrec_out = nrec;
+}
+
+// a group of 16 lanes per stream, 4 streams per wave; spec_mode 2: K1x's streams resume
+__global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_words, uint4 *recs, uint64_t rcap) {
+    constexpr int G = 16, S = 64 / G;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = (int)(threadIdx.x & 63);
+    const int g = lane / G, lj = lane % G;
+    const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(A.hs - 1)));
+    uint32_t *htw = (uint32_t *)smem + (uint32_t)g * table_words;
+    const uint64_t s = (uint64_t)blockIdx.x * S + g;
+    const bool spec = A.spec_mode != 0;
+    bool have = s < A.count;
+    if (have && spec && A.spec[s].flags != 0) have = false;  // finished by K1x
+    const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
+    int32_t n = 0, i = 0, done = 0;
+    const uint8_t *p = blo;
+    if (have) {
+        n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+        p = A.in + A.in_off[s];
+        if (spec) {
+            i = (int32_t)A.spec[s].from;
+            done = (int32_t)A.spec[s].done;
+        }
+    }
+    for (int32_t k = lj; k < (int32_t)A.hs; k += G) htw[k] = have && spec ? A.spec_tab[s * (uint64_t)A.hs + k] : 0u;
+    int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : (have ? 0 : EZ_EINVAL);
+    int32_t nrec = 0;
+    long_loop(p, n, i, done, A.bs, lj, g, htw, hsh, recs + (have ? s * rcap : 0), rcap, blo, bhi, nrec, err);
+    if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
+}
+
 // Edge slots (after the records in the K1 scratch): a zeroed 128-byte dummy region for lane groups
 // without a stream, then kEdgeSlots slots of edge_slot_bytes, then the slot counter (zeroed by the
 // launcher).  A live stream (n >= 4) lacks the 16 bytes before or the 64 after it only if it starts
@@ -780,10 +1058,16 @@ __device__ __forceinline__ void copy_lane(uint8_t *dst, const uint8_t *src, int3
 
 constexpr int32_t kLongLit = 96;  // literals this long are copied by the whole wave
 
+// WIDE: k1_long's 16-byte records, and (spec_mode) the streams K1x hands over: their header and
+// first tokens are written already, the output continues at spec[s].op with the pending literal
+// from spec[s].done; streams K1x finished are skipped
+template <bool WIDE>
 __global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint64_t *recs, uint64_t rcap) {
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t s = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     if (s >= A.count) return;
+    const bool spec = WIDE && A.spec_mode != 0;
+    if (spec && A.spec[s].flags != 0) return;
     const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
     const uint8_t *p = A.in + A.in_off[s];
     const int32_t n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
@@ -797,32 +1081,45 @@ __global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint64_t *r
     const uint64_t *rec = recs + s * rcap;
 
     // header (writer.go:495-517): magic + reset, or reset alone
-    const int32_t H = A.append_magic ? 9 : 3;
-    if (H > cap) {
+    const int32_t H = spec ? (int32_t)A.spec[s].op : (A.append_magic ? 9 : 3);
+    if (!spec && H > cap) {
         if (lane == 0) {
             A.out_size[s] = 0;
             if (A.status) A.status[s] = EZ_ENOSPC;
         }
         return;
     }
-    if (lane == 0) {
+    if (lane == 0 && !spec) {
         const int32_t bsl = (int32_t)__builtin_ctzll((uint64_t)A.bs);
         const uint64_t hm = A.append_magic ? (0x141080797a616502ull << 8 | 0x80) : (0x80ull | 0x10ull << 8 | (uint64_t)bsl << 16);
         const V16 hv{hm, A.append_magic ? (uint64_t)bsl : 0ull};
         put_small(out, hv, (uint32_t)H);
     }
-    int32_t op = H, done = 0;
+    int32_t op = H, done = spec ? (int32_t)A.spec[s].done : 0;
     bool full = false;
     for (int32_t b0 = 0; b0 < m && !full; b0 += 64) {
         const int32_t k = b0 + lane;
         const bool here = k < m;
-        const uint64_t r = here ? rec[k] : 0ull;
-        const int32_t lit_end = (int32_t)(r & 0xfffff), clen = (int32_t)((r >> 20) & 0xfffff), dist = (int32_t)((r >> 40) & 0xfffff);
+        int32_t lit_end, clen, dist;
+        bool forced;
+        if (WIDE) {
+            const uint4 r4 = here ? ((const uint4 *)recs)[s * rcap + (uint64_t)k] : make_uint4(0, 0, 0, 0);
+            lit_end = (int32_t)r4.x;
+            clen = (int32_t)r4.y;
+            dist = (int32_t)r4.z;
+            forced = (r4.w & 1) != 0;
+        } else {
+            const uint64_t r = here ? rec[k] : 0ull;
+            lit_end = (int32_t)(r & 0xfffff);
+            clen = (int32_t)((r >> 20) & 0xfffff);
+            dist = (int32_t)((r >> 40) & 0xfffff);
+            forced = (r >> 60) != 0;
+        }
         const int32_t end = lit_end + clen;
         const int32_t prev = __shfl_up(end, 1, 64);
         const int32_t dk = lane == 0 ? done : prev;
         const int32_t L = lit_end - dk;
-        const bool lit = here && ((r >> 60) != 0 || L > 0);
+        const bool lit = here && (forced || L > 0);
         int32_t ln = 0, tn = 0, on = 0;
         const uint64_t lb = tag_bytes(0x00, L, &ln);
         if (!lit) ln = 0;
@@ -954,7 +1251,7 @@ hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st)
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
-    hipLaunchKernelGGL(k1_emit, dim3(egrid), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
+    hipLaunchKernelGGL(k1_emit<false>, dim3(egrid), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
     return hipGetLastError();
 }
 
@@ -984,7 +1281,7 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
-    hipLaunchKernelGGL(k1_emit, dim3(egrid), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
+    hipLaunchKernelGGL(k1_emit<false>, dim3(egrid), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
     return hipGetLastError();
 }
 
@@ -999,6 +1296,17 @@ __global__ void k_lds_store_order(uint32_t *res) {
     t[l & 7] = (uint16_t)(l + 1);
     __syncthreads();
     if (l < 8 && t[l] != (uint16_t)(56 + l + 1)) atomicAdd(res, 1u);
+}
+
+// the same for 32-bit stores (k1_long's u32 table)
+__global__ void k_lds_store_order32(uint32_t *res) {
+    __shared__ uint32_t t[8];
+    const uint32_t l = threadIdx.x;
+    if (l < 8) t[l] = 0;
+    __syncthreads();
+    t[l & 7] = l + 1;
+    __syncthreads();
+    if (l < 8 && t[l] != 56 + l + 1) atomicAdd(res, 1u);
 }
 
 // The property T32 relies on, checked once per process on the device: same-address LDS
@@ -1043,6 +1351,32 @@ bool lds_exchange_in_lane_order() {
 bool lds_store_in_lane_order() {
     static const bool ok = lds_probe(k_lds_store_order);
     return ok;
+}
+
+bool lds_store32_in_lane_order() {
+    static const bool ok = lds_probe(k_lds_store_order32);
+    return ok;
+}
+
+// K1L: long fresh single-Write streams (table <= 4096 entries, positions < 2^31, LDS lane order);
+// EZ_K1L=0 turns it off (A/B: K1x's continuation on the general kernel)
+bool long_applies(const CompressArgs &a) {
+    static const bool off = getenv("EZ_K1L") && atoi(getenv("EZ_K1L")) == 0;
+    return !off && !a.ring && !a.write_idx && a.start == 0 && a.header && a.hs <= 4096 && a.hs >= 4 && a.max_len > 0 &&
+           a.max_len < (1ull << 31) && lds_store32_in_lane_order();
+}
+uint64_t long_scratch_bytes(const CompressArgs &a) { return a.count * rec_cap(a) * sizeof(WideRec); }
+
+hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
+    constexpr int S = 4;
+    const uint64_t rcap = rec_cap(a);
+    const size_t lds = (size_t)S * (size_t)a.hs * 4;
+    const unsigned grid = (unsigned)((a.count + S - 1) / S);
+    hipLaunchKernelGGL(k1_long, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k1_emit<true>, dim3((unsigned)((a.count + 3) / 4)), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
+    return hipGetLastError();
 }
 
 // the table the batch takes: 16 (T16), 32 (T32) or 0 (K1s cannot take it)

@@ -115,6 +115,10 @@ hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipSt
 // the K1 kernel a batch launch takes: 's' K1s (parse + token writer), 'w' general wave per stream
 char compress_variant(const CompressArgs &a);
 void select_compress_variant(int v);  // 0 = automatic, else a variant letter (tests, A/B)
+// K1L: the lean parse for long fresh streams (ez_compress_split.hip); resumes K1x's streams (spec_mode 2)
+bool long_applies(const CompressArgs &a);
+uint64_t long_scratch_bytes(const CompressArgs &a);
+hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t s);
 // K1x: the data-parallel first pass for long fresh single-Write streams (ez_compress_spec.hip)
 bool spec_applies(const CompressArgs &a, bool any_len = false);  // any_len: also below 64 KiB (forced)
 uint64_t spec_scratch_bytes(const CompressArgs &a);

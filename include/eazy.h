@@ -191,7 +191,8 @@ int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *works
 int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t count);
 /* Testing / A-B measurement (no reference counterpart): force the K1 kernel of
  * later batch calls in this process ('s' K1s, 'S' K1s with the u32
- * exchange table, 'w' general alone, 'x' K1x at any stream length; 0 = automatic choice).  A forced kernel that cannot take a batch falls
+ * exchange table, 'w' general alone, 'x' K1x at any stream length, 'l' K1L alone (the lean
+ * parse for long fresh streams, which otherwise continues K1x's dense streams); 0 = automatic choice).  A forced kernel that cannot take a batch falls
  * back to the automatic choice.  Not thread-safe against concurrent calls. */
 int ez_select_compress_kernel(int kind);
 /* Testing / A-B measurement: the first K2 kernel of later batch decodes with a

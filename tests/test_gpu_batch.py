@@ -13,12 +13,13 @@ pytestmark = pytest.mark.gpu
 MiB = 1 << 20
 
 
-@pytest.fixture(params=["", "S", "w", "x"], ids=["auto", "split32", "general", "k1x"], autouse=True)
+@pytest.fixture(params=["", "S", "w", "x", "l"], ids=["auto", "split32", "general", "k1x", "k1l"], autouse=True)
 def k1_kind(request):
     """Every batch test runs on the automatic K1 choice (K1s: the lean parse on the u16
     table at these shapes), on K1s with the u32 exchange table forced, on the
-    general wave-per-stream kernel forced, and on K1x's rounds forced (where a batch
-    qualifies: fresh single Writes, table <= 4096 entries)."""
+    general wave-per-stream kernel forced, on K1x's rounds forced and on K1L (the lean
+    parse with the window's ring semantics) forced (where a batch qualifies: fresh single
+    Writes, table <= 4096 entries)."""
     import eazy_amd as ez
 
     ez.select_compress_kernel(request.param)
@@ -165,7 +166,7 @@ def test_split_kernel_selected(cuda, k1_kind):
     assert ez.compress_kernel(MiB, 1024, 4096, 65536) == want
     assert ez.compress_kernel(MiB, 1 << 13, 4096, 65536) == "w"  # tables over 4096 entries: the general kernel
     # 2n > block: K1x's rounds, then the general kernel (forced 'w': the general kernel alone)
-    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) == ("w" if k1_kind == "w" else "x")
+    assert ez.compress_kernel(MiB, 1024, 1 << 20, 4) == {"w": "w", "l": "l"}.get(k1_kind, "x")
     assert ez.compress_kernel(MiB, 1 << 13, 1 << 20, 4) == "w"
 
 
