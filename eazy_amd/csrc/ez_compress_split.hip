@@ -1371,6 +1371,11 @@ hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
     constexpr int S = 4;
     const uint64_t rcap = rec_cap(a);
     const size_t lds = (size_t)S * (size_t)a.hs * 4;
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void *)k1_long, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_done = true;
+    }
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     hipLaunchKernelGGL(k1_long, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap);
     hipError_t e = hipGetLastError();
