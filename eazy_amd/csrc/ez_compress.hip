@@ -715,7 +715,7 @@ char compress_variant(const CompressArgs &a) {
     int &forced = g_forced_variant;
     if (forced < 0) {
         const char *e = getenv("EZ_K1");
-        forced = e && std::string(e) == "general" ? 'w' : 0;
+        forced = e && std::string(e) == "general" ? 'w' : (e && std::string(e) == "long" ? 'l' : 0);
     }
     if (forced == 'w') return 'w';
     if (forced == 'l' && long_applies(a)) return 'l';  // K1L alone (tests, A/B)

@@ -1397,11 +1397,17 @@ void select_split_table(bool t32) { g_split_t32 = t32; }
 uint32_t split_stride_words(const CompressArgs &a) { return split_table(a) != 0 ? 1u : 0u; }
 
 // records (8 bytes per record slot entry), then k1_lean's edge area
-uint64_t split_scratch_words(const CompressArgs &a) { return a.count * rec_cap(a) * 2 + (edge_area_bytes(a) + 3) / 4; }
+static bool split_takes_long(const CompressArgs &a) {
+    return !a.write_idx && !split_t32_forced() && split_table(a) != 16 && long_applies(a);
+}
+uint64_t split_scratch_words(const CompressArgs &a) {
+    if (split_takes_long(a)) return (long_scratch_bytes(a) + 3) / 4;
+    return a.count * rec_cap(a) * 2 + (edge_area_bytes(a) + 3) / 4;
+}
 
 // K1s routing: one Write per stream on the u16 table -> k1_lean (EZ_K1S_LEAN=0: k1_parse, the
-// previous form, kept for A/B); multi-Write streams and the u32 table (streams over 64 KiB, or
-// forced) -> k1_parse, 32 lanes per stream for batches of few streams
+// previous form, kept for A/B); one Write per stream on the u32 table (streams over 64 KiB) -> K1L;
+// multi-Write streams and forced T32 -> k1_parse, 32 lanes per stream for batches of few streams
 hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipStream_t st) {
     uint64_t *recs = (uint64_t *)scratch;
     const int T = split_table(a);
@@ -1411,6 +1417,8 @@ hipError_t launch_compress_split(const CompressArgs &a, uint32_t *scratch, hipSt
         return launch_split_g<16, false, true>(a, recs, st);
     }
     if (T == 16) return split_lean() ? launch_lean(a, recs, st) : launch_split_g<16, true, false>(a, recs, st);
+    // single Writes on the u32 table (streams over 64 KiB, C2): K1L, the lean parse (C2 31.5 vs 33.7 ms)
+    if (split_takes_long(a)) return launch_long(a, (uint8_t *)scratch, st);
     if (split_g32(a.count) == 32) return launch_split_g<32, false, false>(a, recs, st);
     return launch_split_g<16, false, false>(a, recs, st);
 }
