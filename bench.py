@@ -344,6 +344,27 @@ def e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, blo
                     "chunks on three HIP streams, one rank"}
 
 
+def copy_peak(dev, nbytes: int = 1 << 30, reps: int = 5) -> float:
+    """Achievable HBM bandwidth on this box (report both denominators): a
+    device-to-device copy of `nbytes`, read + write bytes per second in GB/s."""
+    import torch
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    t1.record()
+    torch.cuda.synchronize()
+    gbs = 2 * nbytes * reps / (t0.elapsed_time(t1) / 1e3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return gbs
+
+
 def checksum(x, chunk: int = 1 << 26) -> int:
     """Position-weighted byte checksum of a CUDA uint8 tensor (int64 wraparound
     is fine: both sides compute it the same way)."""
@@ -503,6 +524,7 @@ def main():
     comp_bytes = int(poff[-1])
     elapsed, k1, k2, k3, xch = ezd.reduce_max([elapsed, k1, k2, k3, xch], R, dev)  # the job ends with its slowest rank
     (comp_all,) = ezd.reduce_sum([comp_bytes], R, dev)
+    peak_meas = copy_peak(dev) if rank == 0 else None  # after the timed region: the second denominator
 
     ms = elapsed / args.steps * 1e3
     gib_step = count_all * size / 2**30
@@ -554,6 +576,9 @@ def main():
             "traffic_source": traffic_src,
             "source_hash": source_hash(),
             "algorithmic_bytes_per_launch": alg,
+            "achievable_peak": peak_meas,
+            "frac_of_achievable": achieved / peak_meas if peak_meas else None,
+            "achievable_peak_note": "device-to-device copy of 1 GiB on this box (read + write GB/s), the second denominator",
         },
         "cpu_baseline": None,
     }
