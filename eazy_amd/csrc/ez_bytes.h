@@ -61,6 +61,14 @@ EZ_HD V16 ld_clamped(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
     const V16 r = shr16(v, (uint32_t)(d > 0 ? d : 0)), l = shl16(v, (uint32_t)(d < 0 ? -d : 0));
     return d >= 0 ? r : l;
 }
+// ld_clamped for a range known to hold at least 16 bytes (no byte loop in the code)
+EZ_HD V16 ld_clamped16(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
+    const uint8_t *yc = y < lo ? lo : (y > hi - 16 ? hi - 16 : y);
+    const V16 v = ld16v(yc);
+    const int64_t d = y - yc;
+    const V16 r = shr16(v, (uint32_t)(d > 0 ? d : 0)), l = shl16(v, (uint32_t)(d < 0 ? -d : 0));
+    return d >= 0 ? r : l;
+}
 // the low `per` bytes of v (1 <= per < 16) repeated over 16 bytes
 EZ_HD V16 run_pattern(V16 v, uint32_t per) {
     V16 x = per >= 8 ? V16{v.lo, per == 8 ? 0 : v.hi & ((1ull << (8 * (per - 8))) - 1)} : V16{v.lo & ((1ull << (8 * per)) - 1), 0};

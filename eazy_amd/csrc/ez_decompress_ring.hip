@@ -52,7 +52,7 @@ __host__ __device__ __forceinline__ int32_t run_step(uint32_t per) { return (int
 
 // 16 bytes at y of the batch [lo, hi) (bytes from hi on read as 0)
 __host__ __device__ __forceinline__ V16 ld_in(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
-    return y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
+    return y + 16 <= hi ? ld16v(y) : ld_clamped16(y, lo, hi);  // (the batch holds >= 16 bytes: checked)
 }
 __host__ __device__ __forceinline__ V16 ring_ld(const uint8_t *ring, int32_t p) {
     const uint8_t *q = ring + (p & (kRing - 1));
@@ -135,7 +135,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             // copies and long literals load from HBM
             V16 v = patt ? pv : ring_ld(ring, rp);
             if (!patt && !near) {
-                if (from_in ? sp + 16 > in_end : sp < out) v = from_in ? ld_clamped(sp, A.in, in_end) : ld_clamped(sp, out, out + cap);
+                if (from_in ? sp + 16 > in_end : sp < out) v = from_in ? ld_clamped16(sp, A.in, in_end) : ld_clamped16(sp, out, out + cap);
                 else v = ld16v(sp);
             }
             ring_st(ring, dst, v);
