@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU tests, then A/B bench lines: bash gpurun_ab.sh VAR "v1 v2" "c1 c2"
+# GPU tests, then A/B bench lines: bash tools/gpurun/gpurun_ab.sh VAR "v1 v2" "c1 c2"
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/ab
 rm -rf $O && mkdir -p $O

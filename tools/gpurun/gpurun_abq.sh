@@ -1,5 +1,5 @@
 #!/bin/bash
-# quick A/B of bench lines without tests: bash gpurun_abq.sh WORKLOAD "ENV=V ..." "ENV=V ..." ...
+# quick A/B of bench lines without tests: bash tools/gpurun/gpurun_abq.sh WORKLOAD "ENV=V ..." "ENV=V ..." ...
 # (each argument after the workload is one arm: space-separated env settings, or "base"); REPS rounds
 set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/abq
