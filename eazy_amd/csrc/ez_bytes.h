@@ -46,8 +46,9 @@ EZ_HD V16 shl16(V16 v, uint32_t k) {
 // 16 bytes at y, clamped into [lo, hi): bytes outside read as 0 (a range shorter than 16 bytes
 // is read byte by byte: one 16-byte load would leave it)
 EZ_HD V16 ld_clamped(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
-    if (hi - lo < 16) {
+    if (hi - lo < 16) {  // a batch of < 16 bytes: a rolled byte loop (few registers)
         V16 v{0, 0};
+#pragma unroll 1
         for (int t = 0; t < 16; t++) {
             const uint64_t b = (y + t >= lo && y + t < hi) ? y[t] : 0;
             if (t < 8) v.lo |= b << (8 * t);

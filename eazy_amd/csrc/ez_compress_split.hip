@@ -1062,9 +1062,10 @@ constexpr int32_t kLongLit = 96;  // literals this long are copied by the whole 
 // first tokens are written already, the output continues at spec[s].op with the pending literal
 // from spec[s].done; streams K1x finished are skipped
 template <bool WIDE>
-__global__ __launch_bounds__(256) void k1_emit(CompressArgs A, const uint64_t *recs, uint64_t rcap) {
+__global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t *recs, uint64_t rcap) {
     const int lane = (int)(threadIdx.x & 63);
-    const uint64_t s = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    // the wave's stream, wave-uniform (readfirstlane: its per-stream values live in SGPRs)
+    const uint64_t s = (uint64_t)blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     if (s >= A.count) return;
     const bool spec = WIDE && A.spec_mode != 0;
     if (spec && A.spec[s].flags != 0) return;

@@ -88,7 +88,8 @@ __global__ __launch_bounds__(256) void k3_gather(const uint8_t *slots, const uin
     const int lane = lane_id();
     const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / kWave);
     const uint64_t work = count * split;
-    for (uint64_t v = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (threadIdx.x >> 6); v < work; v += waves) {
+    for (uint64_t v = (uint64_t)blockIdx.x * (blockDim.x / kWave) + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+         v < work; v += waves) {
         // virtual wave v = stream s, part j of split: part j moves dwords
         // j*64 .. j*64+63 of every split*64-dword round; part 0 also the
         // head and tail bytes
