@@ -433,7 +433,7 @@ __global__ __launch_bounds__(64, 5) void k1_parse(CompressArgs A, uint32_t strid
 //    own bytes x+1 .. x+4;
 //  * only saturated counts (24 forward / 8 backward with room left) take the cooperative
 //    extension (gext), as a rare branch.
-// Loads of the lean parse carry no bounds logic: every stream the loop reads has 16 readable bytes
+// Loads of the lean parse carry no bounds logic: every stream the loop reads has 64 readable bytes
 // before it and 64 after it (k1_lean copies the few streams at the batch's edges into padded
 // slots first), so each piece is one plain aligned load.
 // (global address space: plain global_load instructions, not flat ones, which would also count
@@ -487,6 +487,77 @@ struct WinDw {
         uint32_t d[9];
 #pragma unroll
         for (int t = 0; t < 9; t++) d[t] = (uint32_t)__builtin_amdgcn_ds_bpermute(src + 4 * t, (int)dw);
+        uint32_t b[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+        w0.lo = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+        w0.hi = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
+        w1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
+        w1.hi = (uint64_t)b[6] | ((uint64_t)b[7] << 32);
+    }
+};
+
+// The window's bytes from a 128-byte region held across windows, with the next one in flight.
+// Lane k of a group holds dwords 2k and 2k+1 of the region [p + cb, p + cb + 128) (one aligned
+// dwordx2 per lane); a window at i reads bytes i-8 .. i+38, so the region serves every window with
+// 0 <= i - 8 - cb <= 80.  Most windows advance by 16 (no accept) or by a short match, so a region
+// serves ~4 of them, and the region 64 bytes further on (f, issued one region switch earlier, after
+// that window's candidate gathers) is usually resident when the parse gets there: the window-bytes
+// load leaves the per-window chain (window bytes -> table -> candidate gather -> decision -> next
+// window) except after long jumps.  Regions never start past bmax (their 128 bytes end at most 64
+// bytes after the stream) nor more than 64 bytes before it: k1_lean's edge slots guarantee both.
+struct WinRoll {
+    uint32_t c0, c1, f0, f1;  // this lane's dwords of the current and the prefetched region
+    int32_t cb, fb, bmax, pm; // region starts relative to p (4-byte aligned addresses); p & 3
+    __device__ __forceinline__ int32_t floor4(int32_t y) const { return y - ((pm + y) & 3); }
+    __device__ __forceinline__ void ld(const uint8_t *p, int32_t b, int lj, uint32_t &d0, uint32_t &d1) const {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        typedef const __attribute__((address_space(1))) u32x2 *gu64p;
+        const u32x2 v = *(gu64p)(p + b + 8 * lj);
+        d0 = v.x;
+        d1 = v.y;
+    }
+    __device__ __forceinline__ void init(const uint8_t *p, int32_t n, int lj, bool live) {
+        pm = (int32_t)((uintptr_t)p & 3);
+        bmax = floor4(n - 64);
+        cb = min(floor4(-8), bmax);
+        fb = min(cb + 64, bmax);
+        c0 = c1 = f0 = f1 = 0;
+        if (live) {
+            ld(p, cb, lj, c0, c1);
+            ld(p, fb, lj, f0, f1);
+        }
+    }
+    // the region for the window at i (group-uniform), after this window's gathers
+    __device__ __forceinline__ void advance(const uint8_t *p, int32_t i, int lj, bool live) {
+        const int32_t y = i - 8;
+        if (live && !(y >= cb && y - cb <= 80)) {
+            if (y >= fb && y - fb <= 80) {
+                cb = fb;
+                c0 = f0;
+                c1 = f1;
+            } else {  // a long jump: the region is loaded on the chain
+                cb = min(floor4(y), bmax);
+                ld(p, cb, lj, c0, c1);
+            }
+            fb = min(cb + 64, bmax);
+            ld(p, fb, lj, f0, f1);
+        }
+    }
+    __device__ __forceinline__ void bytes(int32_t i, int g, int lj, V16 &w0, V16 &w1) const {
+        const uint32_t o = (uint32_t)(i - 8 - cb + lj), q = o >> 2, r = o & 3;
+        const int src = 4 * (16 * g + (int)(q >> 1));
+        uint32_t e[10];
+#pragma unroll
+        for (int t = 0; t < 5; t++) {
+            e[2 * t] = (uint32_t)__builtin_amdgcn_ds_bpermute(src + 4 * t, (int)c0);
+            e[2 * t + 1] = (uint32_t)__builtin_amdgcn_ds_bpermute(src + 4 * t, (int)c1);
+        }
+        // an odd first dword starts one further (bit selects: a ?: on the array became a scratch index)
+        const uint32_t m = 0u - (q & 1);
+        uint32_t d[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) d[t] = (e[t + 1] & m) | (e[t] & ~m);
         uint32_t b[8];
 #pragma unroll
         for (int t = 0; t < 8; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
@@ -585,7 +656,8 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
     bool live = !err && n >= 4;
     int32_t guard = 4 * n + 64;
     V16 w0{0, 0}, w1{0, 0};  // bytes x-8 .. x+7 and x+8 .. x+23 of this lane's position x
-    WinDw wd{0, 0};
+    WinRoll wr;
+    wr.init(p, n, lj, live);
     // the bytes around stream position 0, the candidate of every zero table entry:
     // judged without a load
     V16 z0{0, 0}, z1{0, 0};
@@ -593,9 +665,8 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         bytes32(L, p, 0, z0, z1);
         z0.lo = 0;
     }
-    wd.load(L, p, 0, lj);
     while (__ballot(live) != 0) {
-        wd.bytes(g, lj, w0, w1);
+        wr.bytes(i, g, lj, w0, w1);
         if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
         const int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
         const int32_t x = i + lj;
@@ -704,7 +775,7 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
             i += nvalid;
         }
         if (live && (err || i + 4 > n)) live = false;
-        wd.load(L, p, live ? i : 0, lj);  // the next window's bytes
+        wr.advance(p, i, lj, live);  // the next window's region
     }
     nrec_out = nrec;
 }
@@ -989,11 +1060,12 @@ __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_wor
 
 // Edge slots (after the records in the K1 scratch): a zeroed 128-byte dummy region for lane groups
 // without a stream, then kEdgeSlots slots of edge_slot_bytes, then the slot counter (zeroed by the
-// launcher).  A live stream (n >= 4) lacks the 16 bytes before or the 64 after it only if it starts
-// in the batch's first 16 bytes (at most 4 such streams, each >= 4 bytes) or ends in its last 64
-// (at most 16): 20 slots always suffice.
-constexpr int kEdgeSlots = 24;
-__host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + 16 + 64 + 15) & ~15ull; }
+// launcher).  A live stream (n >= 4) lacks the 64 bytes before or the 64 after it only if it starts
+// in the batch's first 64 bytes (at most 16 such streams, each >= 4 bytes) or ends in its last 64
+// (at most 16): 32 slots always suffice.
+constexpr int kEdgeSlots = 40;
+constexpr int32_t kEdgeBefore = 64;  // readable bytes before a stream (WinRoll's regions), 64 after it
+__host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + kEdgeBefore + 64 + 15) & ~15ull; }
 __host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs &a) { return 128 + kEdgeSlots * edge_slot_bytes(a) + 16; }
 
 __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
@@ -1021,20 +1093,21 @@ __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride
     const bool live = !err && n >= 4;
     uint64_t *rec = recs + (have ? s * rcap : 0);
     const uint8_t *p = live ? src : edge + 16;
-    const bool edge_stream = live && (src - 16 < blo || src + n + 64 > bhi);
+    const bool edge_stream = live && (src - kEdgeBefore < blo || src + n + 64 > bhi);
     if (__ballot(edge_stream) != 0) {
-        // copy each edge stream of the wave into a slot: [16 zero bytes][the stream][64 zero bytes]
+        // copy each edge stream of the wave into a slot: [64 zero bytes][the stream][64 zero bytes]
         int32_t slot = 0;
         if (edge_stream && lj == 0) slot = (int32_t)atomicAdd((uint32_t *)(edge + 128 + kEdgeSlots * edge_slot_bytes(A)), 1u);
         slot = bcast(slot, G * g);
-        if (edge_stream && slot >= kEdgeSlots) {  // cannot happen (20 slots suffice)
+        if (edge_stream && slot >= kEdgeSlots) {  // cannot happen (32 slots suffice)
             err = EZ_ESTUCK;
             p = edge + 16;
         }
         if (edge_stream && !err) {
             uint8_t *d = edge + 128 + (uint64_t)slot * edge_slot_bytes(A);
-            for (int32_t k = lj; k < n + 80; k += G) d[k] = (k >= 16 && k < n + 16) ? src[k - 16] : (uint8_t)0;
-            p = d + 16;
+            for (int32_t k = lj; k < n + kEdgeBefore + 64; k += G)
+                d[k] = (k >= kEdgeBefore && k < n + kEdgeBefore) ? src[k - kEdgeBefore] : (uint8_t)0;
+            p = d + kEdgeBefore;
         }
         __threadfence_block();
     }
