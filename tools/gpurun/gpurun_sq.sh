@@ -12,4 +12,4 @@ for P in "$P1" "$P2" "$P3"; do
   timeout -s KILL 120 rocprofv3 --pmc $P --output-format csv -d $O/p$k -o run -- python3 bench.py --no-cpu --no-e2e --no-gather --steps 2 --warmup 1 $* > $O/p$k.log 2>&1
   rc=$?; echo "pass $k rc=$rc"; [ $rc -eq 0 ] || { tail -5 $O/p$k.log; exit $rc; }
 done
-python3 tools/pmc_sum.py $O/p*/run_counter_collection.csv k1_lean k2_ring k1_emit > $O/sum.txt; cat $O/sum.txt
+python3 tools/pmc_sum.py $O/p*/run_counter_collection.csv ${SQ_KERNELS:-k1_lean k2_ring k1_emit} > $O/sum.txt; cat $O/sum.txt
