@@ -72,6 +72,24 @@ __host__ __device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v
     *(u64_ua *)(ring + r2 + 8) = v.hi;
 }
 
+// The common token forms from the header's first 8 bytes, in 32-bit arithmetic without
+// branches: a 1-byte tag (length 1..123; not padding, not a meta) and, for a copy, a 1..3-byte
+// offset (plain, Off1 or Off2, reader.go:422-472) after an optional long prefix (:394-420).
+// false: another form (k2_parse decides).  D is the copy distance, adv the input bytes taken.
+__host__ __device__ __forceinline__ bool fast_tok(uint64_t lo, int32_t &L, int32_t &adv, uint32_t &D, bool &cp) {
+    const uint32_t w0 = (uint32_t)lo;
+    const uint32_t l7 = w0 & 0x7f;
+    cp = (w0 & 0x80) != 0;
+    L = (int32_t)l7;
+    const bool lng = (w0 & 0xff00) == 0xff00;
+    const uint32_t y = (uint32_t)(lo >> (lng ? 16 : 8));  // the offset's bytes
+    const uint32_t o = y & 0xff;
+    const uint32_t D0 = o < 252 ? o : (o == 252 ? 252 + ((y >> 8) & 0xff) : 508 + ((y >> 8) & 0xffff));
+    D = lng ? D0 : D0 + l7;
+    adv = cp ? 2 + (int32_t)lng + (o < 252 ? 0 : (int32_t)o - 251) : 1 + L;
+    return l7 != 0 && l7 < 124 && (!cp || o < 254);
+}
+
 // decodes stream s with `ring` (kRing + 16 bytes, with 16-byte guards on both sides) as its history; false = hand
 // the stream over (host-compilable: tools/ring_emu.hip runs it on the CPU)
 // fper: iterations between flushes (a power of two <= kMaxFlushPer)
@@ -91,6 +109,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         *(u64_ua *)(ring + k + 8) = 0;
     }
     int32_t i = 0, pos = 0, bsl = -1;  // bsl: log2 of the window after MetaReset (-1: none yet)
+    uint32_t win = 0;                  // the window's size once bsl is set (copies farther hand over)
     V16 h{0, 0};                       // 16 bytes at b + i (the next header)
     if (!slow) h = ld_in(b, A.in, in_end);
     // the token being written: rem bytes at dst from sp (input / HBM output) or from the ring
@@ -102,28 +121,40 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     for (;;) {
         if (rem == 0) {
             if (i >= nb) break;
-            K2Tok t;
-            const int r = k2_parse(h, i, nb, pos, cap, lim32, limit, bsl, t);
-            if (r == kParseHandOver) { slow = true; break; }  // the exact decoder takes the stream
-            const int32_t adv = t.adv;
+            // the common forms branch-free; anything else (padding, metas, long tags and
+            // offsets, a check that fails) takes the full parse, which may hand over
+            int32_t L, adv, j = 1;
+            uint32_t D;
+            bool cp;
+            const bool f = fast_tok(h.lo, L, adv, D, cp) && bsl >= 0 && i + adv <= nb && pos + L <= cap && L <= lim32 && (!cp || D <= win);
+            V16 hv{(h.lo >> 8) | (h.hi << 56), h.hi >> 8};  // the header after a 1-byte tag
+            if (!f) {
+                K2Tok t;
+                const int r = k2_parse(h, i, nb, pos, cap, lim32, limit, bsl, t);
+                if (r == kParseHandOver) { slow = true; break; }  // the exact decoder takes the stream
+                L = t.L;
+                adv = t.adv;
+                j = t.j;
+                D = t.D;
+                cp = t.cp;
+                win = bsl < 0 ? 0u : (bsl >= 30 ? 0xffffffffu : 1u << bsl);
+                hv = shr16(h, (uint32_t)j);
+            }
             {  // the token's state, set by every step (a padding or meta step has L = 0: no move)
-                const int32_t L = t.L;
-                const uint32_t j = (uint32_t)t.j, D = t.D;
-                const bool cp = t.cp;
                 dst = pos;
                 rem = L;
                 pos += L;
                 from_in = !cp;
                 near = cp && D <= kNear;
                 rp = dst - (int32_t)D;
-                sp = cp ? out + rp : b + (i + (int32_t)j);
+                sp = cp ? out + rp : b + (i + j);
                 // zero region (D == 0, reader.go:176-179) or a short-period run: one 16-byte
                 // pattern stored every `step` bytes; a short literal is in the header's 16
                 // bytes already
                 const bool run = cp && D < 16;
-                patt = run || (!cp && (int32_t)j + L <= 16);
+                patt = run || (!cp && j + L <= 16);
                 step = run ? run_step(D) : 16;
-                pv = shr16(h, j);
+                pv = hv;
                 if (run) pv = run_pattern(shr16(ring_ld(ring, dst - 16), 16 - D), D);  // D == 0: zeros
             }
             i += adv;
