@@ -41,6 +41,22 @@ constexpr uint32_t kMaxFlushPer = 16;    // kChunk + 16 * (16 + 1) < kRing
 
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 
+// the compiler's scheduler does not move instructions across this point (device code)
+__host__ __device__ __forceinline__ void sched_fence() {
+#ifdef __HIP_DEVICE_COMPILE__
+    __builtin_amdgcn_sched_barrier(0);
+#endif
+}
+
+// whether c holds on any lane of the wave (the host emulation runs one lane)
+__host__ __device__ __forceinline__ bool any_lane(bool c) {
+#ifdef __HIP_DEVICE_COMPILE__
+    return __builtin_amdgcn_ballot_w64(c) != 0;
+#else
+    return c;
+#endif
+}
+
 // bytes a run of period per (1..15) advances per 16-byte pattern store: the largest
 // multiple of per <= 16 (per 0, the zero region: 16), from a nibble table
 __host__ __device__ constexpr uint64_t run_steps() {
@@ -75,8 +91,10 @@ __host__ __device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v
 // The common token forms from the header's first 8 bytes, in 32-bit arithmetic without
 // branches: a 1-byte tag (length 1..123; not padding, not a meta) and, for a copy, a 1..3-byte
 // offset (plain, Off1 or Off2, reader.go:422-472) after an optional long prefix (:394-420).
-// false: another form (k2_parse decides).  D is the copy distance, adv the input bytes taken.
-__host__ __device__ __forceinline__ bool fast_tok(uint64_t lo, int32_t &L, int32_t &adv, uint32_t &D, bool &cp) {
+// Returns a value < 0 for another form (k2_parse decides); D is the copy distance, adv the
+// input bytes taken.  (Conditions as sign bits of one integer: compares would each become a
+// lane mask and every && a scalar instruction.)
+__host__ __device__ __forceinline__ int32_t fast_tok(uint64_t lo, int32_t &L, int32_t &adv, uint32_t &D, bool &cp) {
     const uint32_t w0 = (uint32_t)lo;
     const uint32_t l7 = w0 & 0x7f;
     cp = (w0 & 0x80) != 0;
@@ -84,10 +102,12 @@ __host__ __device__ __forceinline__ bool fast_tok(uint64_t lo, int32_t &L, int32
     const bool lng = (w0 & 0xff00) == 0xff00;
     const uint32_t y = (uint32_t)(lo >> (lng ? 16 : 8));  // the offset's bytes
     const uint32_t o = y & 0xff;
-    const uint32_t D0 = o < 252 ? o : (o == 252 ? 252 + ((y >> 8) & 0xff) : 508 + ((y >> 8) & 0xffff));
+    const bool w = o >= 252, w2 = o == 253;
+    const uint32_t ext = w2 ? 256 + ((y >> 8) & 0xffff) : (y >> 8) & 0xff;
+    const uint32_t D0 = w ? 252 + ext : o;
     D = lng ? D0 : D0 + l7;
-    adv = cp ? 2 + (int32_t)lng + (o < 252 ? 0 : (int32_t)o - 251) : 1 + L;
-    return l7 != 0 && l7 < 124 && (!cp || o < 254);
+    adv = cp ? 2 + (int32_t)lng + (int32_t)w + (int32_t)w2 : 1 + L;
+    return (L - 1) | (122 - (L - 1)) | (cp ? 253 - (int32_t)o : 0);
 }
 
 // decodes stream s with `ring` (kRing + 16 bytes, with 16-byte guards on both sides) as its history; false = hand
@@ -109,85 +129,126 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         *(u64_ua *)(ring + k + 8) = 0;
     }
     int32_t i = 0, pos = 0, bsl = -1;  // bsl: log2 of the window after MetaReset (-1: none yet)
-    uint32_t win = 0;                  // the window's size once bsl is set (copies farther hand over)
+    int32_t win = 0;                   // the window's size once bsl is set (copies farther hand over)
     V16 h{0, 0};                       // 16 bytes at b + i (the next header)
     if (!slow) h = ld_in(b, A.in, in_end);
+    int32_t hd = 0;  // a header loaded from the batch's last 16 bytes: its shift, applied after the wait
     // the token being written: rem bytes at dst from sp (input / HBM output) or from the ring
     int32_t rem = 0, dst = 0, step = 16, rp = 0, fl = 0;  // fl: output below it is in HBM
     uint32_t it = 0;
     const uint8_t *sp = b;
-    bool from_in = false, patt = false, near = false;
+    bool from_in = false, patt = false, near = false, live = !slow;
     V16 pv{0, 0};
-    for (;;) {
-        if (rem == 0) {
-            if (i >= nb) break;
-            // the common forms branch-free; anything else (padding, metas, long tags and
-            // offsets, a check that fails) takes the full parse, which may hand over
-            int32_t L, adv, j = 1;
-            uint32_t D;
-            bool cp;
-            const bool f = fast_tok(h.lo, L, adv, D, cp) && bsl >= 0 && i + adv <= nb && pos + L <= cap && L <= lim32 && (!cp || D <= win);
-            V16 hv{(h.lo >> 8) | (h.hi << 56), h.hi >> 8};  // the header after a 1-byte tag
-            if (!f) {
+    // The lanes of a wave iterate together; every step is written for all of them with selects,
+    // and the rare work (the full parse, runs, HBM moves, clamped loads) sits behind wave-uniform
+    // tests.  An iteration issues the loads of the current token's move, parses the next token
+    // (for the lanes whose current token ends with this move) and loads the header after it
+    // while those loads are in flight, then stores the move and takes the next token's state: the
+    // parse no longer waits behind the move's HBM read, nor the move behind the parse.
+    // (every lane loads in every iteration; lanes are live only if the batch holds >= 16 bytes)
+    for (bool go = any_lane(live); go; go = any_lane(live)) {
+        if (any_lane(hd != 0)) {
+            if (hd != 0) h = shr16(h, (uint32_t)hd);  // bytes past the batch read 0
+        }
+        // ---- move, part 1: this iteration's bytes of the current token (rem == 0: nothing)
+        V16 v = ring_ld(ring, rp);
+        const bool hb = rem > 0 && !patt && !near;  // a far copy or a long literal: from HBM
+        // every lane issues exactly one load here (the clamped address for a source at the
+        // batch's or the slot's edge, fixed up after the wait; A.in for the others: the batch
+        // holds >= 16 bytes when any lane is live), so the waits can count past it
+        const uint8_t *glo = from_in ? A.in : out, *ghi = from_in ? in_end : out + cap;
+        const uint8_t *gc = !hb ? A.in : (sp < glo ? glo : (sp > ghi - 16 ? ghi - 16 : sp));
+        const V16 graw = ld16v(gc);
+        const int32_t gd = (int32_t)(sp - gc);  // (hb lanes: the clamp's shift)
+        sched_fence();  // the loads above go out before the parse below waits on the header
+        const int32_t kk = rem < step ? rem : step;
+        // ---- parse: the lanes whose current token ends with this move take the next one
+        bool np = live && rem == kk;
+        const bool fin = np && i >= nb;  // the input is done: this move is the lane's last
+        np = np && !fin;
+        // the common forms branch-free; anything else (padding, metas, long tags and
+        // offsets, a check that fails) takes the full parse, which may hand over
+        int32_t L, adv, j = 1;
+        uint32_t D;
+        bool cp;
+        const int32_t ft = fast_tok(h.lo, L, adv, D, cp);
+        const bool f = (ft | bsl | (nb - i - adv) | (cap - pos - L) | (lim32 - L) | (cp ? win - (int32_t)D : 0)) >= 0;
+        V16 hv{(h.lo >> 8) | (h.hi << 56), h.hi >> 8};  // the header after a 1-byte tag
+        bool ho = false;                                // hand the stream over
+        if (any_lane(np && !f)) {
+            if (np && !f) {
                 K2Tok t;
                 const int r = k2_parse(h, i, nb, pos, cap, lim32, limit, bsl, t);
-                if (r == kParseHandOver) { slow = true; break; }  // the exact decoder takes the stream
-                L = t.L;
-                adv = t.adv;
-                j = t.j;
-                D = t.D;
-                cp = t.cp;
-                win = bsl < 0 ? 0u : (bsl >= 30 ? 0xffffffffu : 1u << bsl);
-                hv = shr16(h, (uint32_t)j);
+                if (r == kParseHandOver) {
+                    ho = true;
+                } else {
+                    L = t.L;
+                    adv = t.adv;
+                    j = t.j;
+                    D = t.D;
+                    cp = t.cp;
+                    win = bsl < 0 ? 0 : (bsl >= 30 ? 0x7fffffff : 1 << bsl);  // (D < 2^17 on the fast path)
+                    hv = shr16(h, (uint32_t)j);
+                }
             }
-            {  // the token's state, set by every step (a padding or meta step has L = 0: no move)
-                dst = pos;
-                rem = L;
-                pos += L;
-                from_in = !cp;
-                near = cp && D <= kNear;
-                rp = dst - (int32_t)D;
-                sp = cp ? out + rp : b + (i + j);
-                // zero region (D == 0, reader.go:176-179) or a short-period run: one 16-byte
-                // pattern stored every `step` bytes; a short literal is in the header's 16
-                // bytes already
-                const bool run = cp && D < 16;
-                patt = run || (!cp && j + L <= 16);
-                step = run ? run_step(D) : 16;
-                pv = hv;
-                if (run) pv = run_pattern(shr16(ring_ld(ring, dst - 16), 16 - D), D);  // D == 0: zeros
-            }
-            i += adv;
-            // the next header, loaded beside this token's first move
-            if (i < nb) h = ld_in(b + i, A.in, in_end);
         }
-        if (rem > 0) {
-            // the ring read is taken by every lane (one LDS read, no branch level); only far
-            // copies and long literals load from HBM
-            V16 v = patt ? pv : ring_ld(ring, rp);
-            if (!patt && !near) {
-                if (from_in ? sp + 16 > in_end : sp < out) v = from_in ? ld_clamped16(sp, A.in, in_end) : ld_clamped16(sp, out, out + cap);
-                else v = ld16v(sp);
-            }
-            ring_st(ring, dst, v);
-            const int32_t kk = rem < step ? rem : step;
-            dst += kk;
-            sp += kk;
-            rp += kk;
-            rem -= kk;
+        np = np && !ho;
+        const int32_t i0 = i;
+        i = np ? i + adv : i;
+        // the next header (lanes not parsing reload theirs), one load for every lane: near the
+        // batch's end from its last 16 bytes, shifted after the wait at the next iteration's top
+        const uint8_t *hc = b + i > in_end - 16 ? in_end - 16 : b + i;  // (the batch's last 16 bytes)
+        h = ld16v(hc);
+        hd = (int32_t)(b + i - hc);
+        // ---- move, part 2
+        V16 g = graw;
+        if (any_lane(hb && gd != 0)) {  // bytes outside the batch or before the slot read 0
+            if (hb && gd != 0) g = gd > 0 ? shr16(graw, (uint32_t)gd) : shl16(graw, (uint32_t)-gd);
         }
+        v.lo = hb ? g.lo : v.lo;  // (field by field: a select of the struct went through scratch)
+        v.hi = hb ? g.hi : v.hi;
+        v.lo = patt ? pv.lo : v.lo;
+        v.hi = patt ? pv.hi : v.hi;
+        ring_st(ring, dst, v);
+        dst += kk;
+        sp += kk;
+        rp += kk;
+        rem -= kk;
+        // ---- the next token's state (a padding or meta step has L = 0: no move)
+        const bool run = cp && D < 16;
+        rem = np ? L : rem;
+        from_in = np ? !cp : from_in;
+        near = np ? cp && D <= kNear : near;
+        rp = np ? pos - (int32_t)D : rp;
+        sp = np ? (cp ? out + (pos - (int32_t)D) : b + (i0 + j)) : sp;
+        // zero region (D == 0, reader.go:176-179) or a short-period run: one 16-byte pattern
+        // stored every `step` bytes; a short literal is in the header's 16 bytes already
+        patt = np ? run || (!cp && j + L <= 16) : patt;
+        step = np ? (run ? run_step(D) : 16) : step;
+        pv.lo = np ? hv.lo : pv.lo;
+        pv.hi = np ? hv.hi : pv.hi;
+        if (any_lane(np && run)) {  // (after the store: the pattern's source may be this move's bytes)
+            if (np && run) pv = run_pattern(shr16(ring_ld(ring, pos - 16), 16 - D), D);  // D == 0: zeros
+        }
+        pos = np ? pos + L : pos;
         // finished 128-byte chunks of output leave the ring as whole lines, every fper-th
-        // iteration: the lanes of a wave iterate together, so the flush is one wave-wide
-        // block every fper iterations with many lanes active, not one nearly every
-        // iteration for the few lanes that just finished a chunk (unflushed output stays
-        // below kChunk + 16 * (fper + 1) <= kRing bytes)
+        // iteration: one wave-wide block every fper iterations with many lanes active, not
+        // one nearly every iteration for the few lanes that just finished a chunk (16-byte
+        // pieces stored every iteration, and the fixed store count that lets the waits count
+        // past them, measured slower: 0.75 against 0.57 ms at C1)
+        // (unflushed output stays below kChunk + 16 * (fper + 1) <= kRing bytes)
         if ((++it & (fper - 1)) == 0) {
-            while (dst >= fl + kChunk) {
+            while (any_lane(dst >= fl + kChunk)) {
+                if (dst >= fl + kChunk) {
 #pragma unroll
-                for (int32_t t = 0; t < kChunk; t += 16) st16v(out + fl + t, ring_ld(ring, fl + t));
-                fl += kChunk;
+                    for (int32_t t = 0; t < kChunk; t += 16) st16v(out + fl + t, ring_ld(ring, fl + t));
+                    fl += kChunk;
+                }
             }
         }
+        slow = slow || ho;
+        rem = ho ? 0 : rem;
+        live = live && !fin && !ho;
     }
     if (!slow) {  // the last partial chunk, exact bytes
         int32_t q = fl;
