@@ -139,6 +139,11 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     const uint8_t *sp = b;
     bool from_in = false, patt = false, near = false, live = !slow;
     V16 pv{0, 0};
+    // (a load after the first header, as every iteration ends with one after the next header:
+    // the loop's entry then matches its back edge and the header wait counts past it; the
+    // offset table holds >= 16 bytes)
+    V16 graw = ld16v((const uint8_t *)A.in_off);
+    int32_t gd = 0;
     // The lanes of a wave iterate together; every step is written for all of them with selects,
     // and the rare work (the full parse, runs, HBM moves, clamped loads) sits behind wave-uniform
     // tests.  An iteration issues the loads of the current token's move, parses the next token
@@ -150,17 +155,10 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         if (any_lane(hd != 0)) {
             if (hd != 0) h = shr16(h, (uint32_t)hd);  // bytes past the batch read 0
         }
-        // ---- move, part 1: this iteration's bytes of the current token (rem == 0: nothing)
+        // ---- move, part 1: this iteration's bytes of the current token (rem == 0: nothing);
+        // a far copy's or long literal's 16 bytes (graw) were loaded one iteration ago
         V16 v = ring_ld(ring, rp);
         const bool hb = rem > 0 && !patt && !near;  // a far copy or a long literal: from HBM
-        // every lane issues exactly one load here (the clamped address for a source at the
-        // batch's or the slot's edge, fixed up after the wait; A.in for the others: the batch
-        // holds >= 16 bytes when any lane is live), so the waits can count past it
-        const uint8_t *glo = from_in ? A.in : out, *ghi = from_in ? in_end : out + cap;
-        const uint8_t *gc = !hb ? A.in : (sp < glo ? glo : (sp > ghi - 16 ? ghi - 16 : sp));
-        const V16 graw = ld16v(gc);
-        const int32_t gd = (int32_t)(sp - gc);  // (hb lanes: the clamp's shift)
-        sched_fence();  // the loads above go out before the parse below waits on the header
         const int32_t kk = rem < step ? rem : step;
         // ---- parse: the lanes whose current token ends with this move take the next one
         bool np = live && rem == kk;
@@ -249,6 +247,18 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         slow = slow || ho;
         rem = ho ? 0 : rem;
         live = live && !fin && !ho;
+        // the HBM source of the next iteration's move, loaded now (every lane one load: the
+        // clamped address for a source at the batch's or the slot's edge, fixed up after the
+        // wait; A.in for the others, the batch holds >= 16 bytes when any lane is live), so the
+        // next iteration's parse and header load run while it is in flight
+        {
+            const bool hn = rem > 0 && !patt && !near;
+            const uint8_t *glo = from_in ? A.in : out, *ghi = from_in ? in_end : out + cap;
+            const uint8_t *gc = !hn ? A.in : (sp < glo ? glo : (sp > ghi - 16 ? ghi - 16 : sp));
+            graw = ld16v(gc);
+            gd = (int32_t)(sp - gc);  // (hn lanes: the clamp's shift)
+            sched_fence();            // (issued here, not sunk to the next iteration's parse)
+        }
     }
     if (!slow) {  // the last partial chunk, exact bytes
         int32_t q = fl;
