@@ -269,7 +269,13 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         const char *v = getenv("EZ_K2");
         g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w' : (v && strcmp(v, "ring") == 0 ? 'r' : 0);
     }
-    if (g_decompress_variant == 'w' || (g_decompress_variant == 0 && a.max_out >= long_slot)) {
+    // K2w for long slots, unless the batch holds enough streams for K2r's lane per stream to
+    // outrun K2w's wave per stream (1 GiB batches: 16 Ki x 64 KiB 147 vs 101 GiB/s for K2r,
+    // 8 Ki x 128 KiB 74 vs 88; streams past 256 KiB stay on K2w, whose wave takes a long stream
+    // ~2x faster than one lane)
+    static const uint64_t ring_min = getenv("EZ_K2_RING_MIN") ? (uint64_t)atoll(getenv("EZ_K2_RING_MIN")) : 12288u;
+    const bool ring_ok = a.count >= ring_min && a.max_out <= (256u << 10);
+    if (g_decompress_variant == 'w' || (g_decompress_variant == 0 && a.max_out >= long_slot && !ring_ok)) {
         // long streams (slots of 64 KiB and more, C2/C4): too few to give every lane one;
         // K2w gives each a wave, and its hand-overs go to the exact decoder; the long literals
         // it defers are moved last (the exact decoder writes the same bytes for a stream it takes)
