@@ -1029,16 +1029,19 @@ __device__ __forceinline__ void long_loop(const uint8_t *p, int32_t n, int32_t i
 }
 
 // a group of 16 lanes per stream, 4 streams per wave; spec_mode 2: K1x's streams resume
-__global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_words, uint4 *recs, uint64_t rcap) {
-    constexpr int G = 16, S = 64 / G;
+// spw: streams per wave (1, 2 or 4; the other lane groups idle, with no table): a batch of few long
+// streams runs more waves per SIMD, each a lone latency chain, instead of fewer waves of 4 streams
+__global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_words, uint4 *recs, uint64_t rcap, uint32_t spw) {
+    constexpr int G = 16;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = (int)(threadIdx.x & 63);
     const int g = lane / G, lj = lane % G;
+    const bool grp = (uint32_t)g < spw;
     const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(A.hs - 1)));
-    uint32_t *htw = (uint32_t *)smem + (uint32_t)g * table_words;
-    const uint64_t s = (uint64_t)blockIdx.x * S + g;
+    uint32_t *htw = (uint32_t *)smem + (uint32_t)(grp ? g : 0) * table_words;  // (an idle group never touches it)
+    const uint64_t s = (uint64_t)blockIdx.x * spw + (uint32_t)g;
     const bool spec = A.spec_mode != 0;
-    bool have = s < A.count;
+    bool have = grp && s < A.count;
     if (have && spec && A.spec[s].flags != 0) have = false;  // finished by K1x
     const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
     int32_t n = 0, i = 0, done = 0;
@@ -1051,7 +1054,8 @@ __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_wor
             done = (int32_t)A.spec[s].done;
         }
     }
-    for (int32_t k = lj; k < (int32_t)A.hs; k += G) htw[k] = have && spec ? A.spec_tab[s * (uint64_t)A.hs + k] : 0u;
+    if (grp)
+        for (int32_t k = lj; k < (int32_t)A.hs; k += G) htw[k] = have && spec ? A.spec_tab[s * (uint64_t)A.hs + k] : 0u;
     int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : (have ? 0 : EZ_EINVAL);
     int32_t nrec = 0;
     long_loop(p, n, i, done, A.bs, lj, g, htw, hsh, recs + (have ? s * rcap : 0), rcap, blo, bhi, nrec, err);
@@ -1442,7 +1446,11 @@ bool long_applies(const CompressArgs &a) {
 uint64_t long_scratch_bytes(const CompressArgs &a) { return a.count * rec_cap(a) * sizeof(WideRec); }
 
 hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
-    constexpr int S = 4;
+    // streams per wave: one while a wave per stream still leaves at most one wave per SIMD (C4s'
+    // 64 streams: K1 361 -> 291 ms), else 4 (each wave's instructions serve 4 streams; C2's 4,096
+    // streams: 32.3 ms at 4, 33.5 at 2, 38.2 at 1); EZ_K1L_SPW=1|2|4 overrides
+    static const uint32_t spw_env = getenv("EZ_K1L_SPW") ? (uint32_t)atoi(getenv("EZ_K1L_SPW")) : 0u;
+    const uint32_t S = spw_env == 1 || spw_env == 2 || spw_env == 4 ? spw_env : (a.count <= 1024 ? 1u : 4u);
     const uint64_t rcap = rec_cap(a);
     const size_t lds = (size_t)S * (size_t)a.hs * 4;
     static bool attr_done = false;
@@ -1451,7 +1459,7 @@ hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
         attr_done = true;
     }
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
-    hipLaunchKernelGGL(k1_long, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap);
+    hipLaunchKernelGGL(k1_long, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k1_emit<true>, dim3((unsigned)((a.count + 3) / 4)), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
