@@ -99,6 +99,20 @@ def test_ragged_and_edge_lengths(cuda):
     _check(cuda, bufs)
 
 
+def test_many_streams_k1l_and_long_slots(cuda):
+    """Batches past 1,024 streams: K1L (when forced) runs 4 streams per wave, below 1,024
+    one; and >= 12,288 streams with 64 KiB slots take the lane-per-stream decoder K2r by
+    default (K2w below), both checked against the oracle and the exact decoder."""
+    from eazy_amd import synth
+
+    d = synth.logs(29, 1100 * 3000).tobytes()
+    _check(cuda, [d[k * 3000 : (k + 1) * 3000] for k in range(1100)])
+    # 12,288 streams, one of them 64 KiB: the slots hint (max_len) is >= 64 KiB
+    small = synth.logs(31, 12287 * 64 + 65536).tobytes()
+    bufs = [small[k * 64 : (k + 1) * 64] for k in range(12287)] + [small[12287 * 64 :]]
+    _check(cuda, bufs)
+
+
 def test_small_windows_and_tables(cuda):
     from eazy_amd import synth
 
