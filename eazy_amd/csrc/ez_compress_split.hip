@@ -1446,11 +1446,11 @@ bool long_applies(const CompressArgs &a) {
 uint64_t long_scratch_bytes(const CompressArgs &a) { return a.count * rec_cap(a) * sizeof(WideRec); }
 
 hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
-    // streams per wave: one while a wave per stream still leaves at most one wave per SIMD (C4s'
-    // 64 streams: K1 361 -> 291 ms), else 4 (each wave's instructions serve 4 streams; C2's 4,096
-    // streams: 32.3 ms at 4, 33.5 at 2, 38.2 at 1); EZ_K1L_SPW=1|2|4 overrides
+    // streams per wave: one for batches of a few hundred streams (C4s' 64: K1 361 -> 291 ms), else 4
+    // (each wave's instructions serve 4 streams; C2's 4,096 streams: 32.3 ms at 4, 33.5 at 2, 38.2 at
+    // 1; 1,024 x 1 MiB compressed at 7.3 GiB/s at 1 against 7.6 at 4); EZ_K1L_SPW=1|2|4 overrides
     static const uint32_t spw_env = getenv("EZ_K1L_SPW") ? (uint32_t)atoi(getenv("EZ_K1L_SPW")) : 0u;
-    const uint32_t S = spw_env == 1 || spw_env == 2 || spw_env == 4 ? spw_env : (a.count <= 1024 ? 1u : 4u);
+    const uint32_t S = spw_env == 1 || spw_env == 2 || spw_env == 4 ? spw_env : (a.count <= 256 ? 1u : 4u);
     const uint64_t rcap = rec_cap(a);
     const size_t lds = (size_t)S * (size_t)a.hs * 4;
     static bool attr_done = false;

@@ -100,7 +100,7 @@ def test_ragged_and_edge_lengths(cuda):
 
 
 def test_many_streams_k1l_and_long_slots(cuda):
-    """Batches past 1,024 streams: K1L (when forced) runs 4 streams per wave, below 1,024
+    """Batches past 256 streams: K1L (when forced) runs 4 streams per wave, up to 256
     one; and >= 12,288 streams with 64 KiB slots take the lane-per-stream decoder K2r by
     default (K2w below), both checked against the oracle and the exact decoder."""
     from eazy_amd import synth
