@@ -44,6 +44,7 @@ namespace {
 constexpr int64_t kChunk = 16384;     // positions per kx_pred chunk (chunk-local distances fit u16)
 constexpr uint32_t kNone = 0xffffffffu;
 constexpr int64_t kPiece = 256;       // kx_judge: positions per block step
+static_assert(kChunk % kPiece == 0, "kx_judge reads one kx_pred chunk's table per piece");
 constexpr int64_t kCopyPiece = 65536; // kx_copy: bytes per block step
 constexpr int kRounds = 8;            // rounds before the general kernel takes the rest (EZ_K1X_ROUNDS)
 
@@ -201,47 +202,48 @@ __device__ __forceinline__ V16 ld16_al(const uint8_t *y, const uint8_t *lo, cons
     return V16{(uint64_t)e0 | ((uint64_t)e1 << 32), (uint64_t)e2 | ((uint64_t)e3 << 32)};
 }
 
-// vx = stream bytes x-8 .. x+7
-__device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t *p, int64_t n, int64_t x, int64_t cand, int64_t done,
-                                           const V16 vx) {
-    const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
+// vx = stream bytes x-8 .. x+7.  Positions in 32 bits (K1x takes streams under 2 GiB): the
+// judgement is most of K1x's time and every 64-bit compare or min is two instructions; only the
+// window size bs stays 64-bit
+__device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t *p, int32_t n, int32_t x, int32_t cand, int32_t done,
+                                           const V16 vx, const uint8_t *lo, const uint8_t *hi) {
     const int64_t bs = A.bs;
     if (cand >= done && x > cand) {
         // off >= 0 and i > done + off: writeRunlen with st = cand (writer.go:227-231, 441-473)
         const V16 vc = ld16_al(p + cand - 8, lo, hi);
         if (cand + 8 < n && vc.hi == 0) return true;  // writeZeros: >= 8 zeros at st
         const uint64_t df = vx.hi ^ vc.hi, db = vx.lo ^ vc.lo;
-        int64_t f = df ? (int64_t)(__builtin_ctzll(df) >> 3) : 8;
+        int32_t f = df ? (int32_t)(__builtin_ctzll(df) >> 3) : 8;
         f = f < n - x ? f : n - x;
-        int64_t c = db ? (int64_t)(__builtin_clzll(db) >> 3) : 8;
-        const int64_t cl = cand < x - done ? cand : x - done;
+        int32_t c = db ? (int32_t)(__builtin_clzll(db) >> 3) : 8;
+        const int32_t cl = cand < x - done ? cand : x - done;
         c = c < cl ? c : cl;
         return f + c >= kMinCopyChunk;  // a run or the cut branch: both emit
     }
-    if (done - cand > bs) return false;  // far skip (writer.go:221-224)
+    if ((int64_t)(done - cand) > bs) return false;  // far skip (writer.go:221-224)
     // window match against the ring image at w.pos = done (writer.go:233-301): block[y & mask]
     // holds stream byte done - bs + ((y - done) & mask), zero before the stream
     V16 vc;
-    if (cand - 8 >= 0 && cand - 8 >= done - bs && cand + 8 <= done) {
+    if (cand - 8 >= 0 && (int64_t)cand - 8 >= (int64_t)done - bs && cand + 8 <= done) {
         vc = ld16_al(p + cand - 8, lo, hi);
     } else {
         vc = V16{0, 0};
         const int64_t mask = bs - 1;
         for (int t = 0; t < 16; t++) {
-            const int64_t q = done - bs + ((cand - 8 + t - done) & mask);
+            const int64_t q = (int64_t)done - bs + (((int64_t)cand - 8 + t - done) & mask);
             const uint64_t b = q >= 0 ? p[q] : 0;
             if (t < 8) vc.lo |= b << (8 * t);
             else vc.hi |= b << (8 * (t - 8));
         }
     }
     const uint64_t df = vx.hi ^ vc.hi, db = vx.lo ^ vc.lo;
-    int64_t f = df ? (int64_t)(__builtin_ctzll(df) >> 3) : 8;
+    int32_t f = df ? (int32_t)(__builtin_ctzll(df) >> 3) : 8;
     f = f < n - x ? f : n - x;
-    int64_t c = db ? (int64_t)(__builtin_clzll(db) >> 3) : 8;
+    int32_t c = db ? (int32_t)(__builtin_clzll(db) >> 3) : 8;
     c = c < x - done ? c : x - done;
     // the two trims (writer.go:280-291): the copy stays within bs of x and ends by w.pos
     int64_t len = f + c;
-    const int64_t t1 = bs - (x - cand), t2 = done - cand + c;
+    const int64_t t1 = bs - (int64_t)(x - cand), t2 = (int64_t)(done - cand + c);
     len = len < t1 ? len : t1;
     len = len < t2 ? len : t2;
     return len >= kMinCopyChunk;
@@ -261,17 +263,21 @@ __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
     for (uint64_t q = blockIdx.x; q < nact * kp; q += gridDim.x) {
         const uint64_t j = q / nact, s = B.act[q % nact];
         const SpecState sp = A.spec[s];
-        const int64_t n = slen(A, s), from = sp.from, done = sp.done;
-        const int64_t xb = (from & ~(kPiece - 1)) + (int64_t)j * kPiece;
+        const int32_t n = (int32_t)slen(A, s), from = (int32_t)sp.from, done = (int32_t)sp.done;  // (< 2 GiB)
+        const int32_t xb = (from & ~(kPiece - 1)) + (int32_t)j * kPiece;
         if (xb + 4 > n) continue;  // uniform: the block's values only
         const uint8_t *p = A.in + A.in_off[s];
+        // the piece's rows, block-uniform (a piece never straddles a kx_pred chunk: both aligned)
+        const uint16_t *prow = B.pred + (A.in_off[s] - A.in_off[0]);
+        const uint32_t *trow = B.tabs + (s * B.kmax + (uint64_t)(xb / kChunk)) * (uint64_t)A.hs;
+        const uint32_t *srow = A.spec_tab + s * (uint64_t)A.hs;
         // stage bytes [xb - 8, xb + kPiece + 24) by coalesced aligned words (outside the batch: 0);
         // whether an accept before the piece is known already is read once, by thread 0 (another
         // block's atomicMin may land between two threads' reads: the decision must be the block's)
         const uint8_t *wa = (const uint8_t *)((uintptr_t)(p + xb - 8) & ~(uintptr_t)3);
         const uint32_t r0 = (uint32_t)((uintptr_t)(p + xb - 8) & 3);
         __syncthreads();  // the previous piece's readers are done
-        if (threadIdx.x == 0) skip = xb > (int64_t)__atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
+        if (threadIdx.x == 0) skip = (int64_t)xb > (int64_t)__atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
         if (threadIdx.x < kPiece / 4 + 8) {
             const uint8_t *w = wa + 4 * threadIdx.x;
             uint32_t v = 0;
@@ -283,7 +289,7 @@ __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
         }
         __syncthreads();
         if (skip) continue;
-        const int64_t x = xb + threadIdx.x;
+        const int32_t x = xb + (int32_t)threadIdx.x;
         bool acc = false;
         if (x >= from && x + 4 <= n) {
             const uint32_t o = r0 + threadIdx.x, k = o >> 2, r = o & 3;
@@ -291,12 +297,12 @@ __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
             const V16 vx{(uint64_t)__builtin_amdgcn_alignbyte(d1, d0, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32),
                          (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, r) << 32)};
             const uint32_t h = ((uint32_t)vx.hi * kHashMul) >> hsh;
-            const uint16_t d = B.pred[A.in_off[s] - A.in_off[0] + x];
+            const uint16_t d = prow[x];
             // nearest earlier same-hash position (chunk-local, else the chunk's incoming entry);
             // before `from` the table at `from` holds the entry
-            const int64_t pc = d ? x - d : (int64_t)B.tabs[(s * B.kmax + (uint64_t)(x / kChunk)) * (uint64_t)A.hs + h];
-            const int64_t cand = pc >= from ? pc : (int64_t)A.spec_tab[s * (uint64_t)A.hs + h];
-            acc = kx_accepts(A, p, n, x, cand, done, vx);
+            const int32_t pc = d ? x - d : (int32_t)trow[h];
+            const int32_t cand = pc >= from ? pc : (int32_t)srow[h];
+            acc = kx_accepts(A, p, n, x, cand, done, vx, lo, hi);
         }
         const uint64_t m = wballot(acc);
         if (m && lane == ffs64(m)) atomicMin(&B.first[s], (uint32_t)x);
