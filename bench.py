@@ -13,7 +13,8 @@ payload to rank 0 is timed separately ("gather").  value = uncompressed GiB
 processed by all ranks per second (GiB = 2^30 B).
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
-       (N>1 via python -m torch.distributed.run --nproc-per-node N bench.py --gpus N)
+       (N>1: under python -m torch.distributed.run --nproc-per-node N bench.py --gpus N, or
+        bench.py --gpus N alone, which starts that launcher as a child process itself)
 """
 
 from __future__ import annotations
@@ -86,7 +87,30 @@ def parse():
                     help="PMC-derived HBM bytes per launch (tools/traffic.py); default: the committed "
                          "profiles/traffic_<workload>.json when its kernel-source hash and shape match this run")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the timed payload gather to rank 0")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="CPU rehearsal of the N-rank launch and exchange (gloo, no kernels: each stream's payload is "
+                         "its raw bytes); prints one JSON line with no throughput claim")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc: int, argv: list[str]) -> int:
+    """`python bench.py --gpus N` (N > 1) outside torch.distributed.run: start
+    N ranks as ONE child process tree (torch.distributed.run, 127.0.0.1
+    rendezvous) before anything here touches the GPU, let rank 0's JSON line
+    through on the inherited stdout, and return the child's exit code."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + argv
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
 def source_hash() -> str:
@@ -421,8 +445,50 @@ def gather_check(ez, ezd, R, packed, goff, count_all, first_all, data, size, dev
                     "every rank's range against that rank's input checksum"}
 
 
+def rehearse(args, R):
+    """CPU rehearsal of the sharded path (`--rehearse`, gloo): the same
+    launch, shard split, size all-gather, global offsets and payload gather as
+    the GPU run, with every stream's payload its own bytes (no kernels, no
+    oracle).  Rank 0 checks the gathered batch equals the global input."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from eazy_amd import dist as ezd
+    from eazy_amd import synth
+
+    if R.world > 1:
+        dist.init_process_group("gloo")
+    count_all, size = (args.streams or 4096), (args.stream_bytes or 4096)
+    first, last = ezd.shard_range(count_all, R)
+    mine = torch.from_numpy(synth.global_logs(1000, first, last, size).copy())
+    sizes = torch.full((last - first,), size, dtype=torch.int64)
+    goff = ezd.global_offsets(ezd.exchange_sizes(sizes, count_all, R))
+    assert int(goff[first]) == first * size and int(goff[last]) == last * size, "global offsets"
+    out = ezd.gather_payload(mine, goff, count_all, R)
+    total = ezd.reduce_sum([mine.numel()], R)[0]
+    if R.is_root:
+        want = synth.global_logs(1000, 0, count_all, size)
+        assert total == count_all * size and np.array_equal(out.numpy(), want), "gathered batch differs"
+        print(json.dumps({"metric": "rehearsal (CPU, gloo, no kernels)", "value": None, "n_gpus": R.world,
+                          "streams_total": count_all, "streams_per_rank": ezd.shard_counts(count_all, R.world),
+                          "bytes_gathered": int(goff[-1]), "gathered_equals_input": True}), flush=True)
+    if R.world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    from eazy_amd import dist as ezd
+
+    R = ezd.from_env()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    if args.gpus != R.world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but the launch has {R.world} rank(s) (WORLD_SIZE)")
+    if args.rehearse:
+        return rehearse(args, R)
+
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -430,9 +496,6 @@ def main():
     import eazy_amd as ez
     from eazy_amd import synth
 
-    from eazy_amd import dist as ezd
-
-    R = ezd.from_env()
     world, rank, local = R.world, R.rank, R.local
     if world > 1:
         dist.init_process_group("nccl")
@@ -591,7 +654,7 @@ def main():
         if count >= 2 * args.e2e_chunks:
             res["e2e"]["pipelined"] = e2e_pipelined(ez, data, off, offs, cb, packed, poff, dws, out, osz, ost, block, htable,
                                                     size, total, comp_bytes, chunks=args.e2e_chunks)
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if rank == 0 and not args.no_cpu:  # N > 1: rank 0's shard (the other ranks' streams are alike)
         cb_res, checked = cpu_baseline(host, offs, block, htable, args.cpu_seconds, packed.cpu().numpy(), poff.cpu().numpy())
         res["cpu_baseline"] = cb_res
         res["parity"] = {"streams_byte_compared_with_oracle": checked, "streams": count,

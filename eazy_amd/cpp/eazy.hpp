@@ -30,6 +30,7 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <cstdio>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -75,10 +76,30 @@ enum class Err : int {
 
 inline const char *ErrString(Err e) { return ez_strerror((int)e); }
 
-// What Go does with panic(): invalid sizes, impossible lengths, bad meta.
+// What Go does with panic(): invalid sizes, impossible lengths, bad meta.  what() is the
+// reference's panic value (writer.go:163, 167, 309, 562, 596); Encoder.Meta panics with the
+// meta int itself (writer.go:601): then has_value and value hold it, and what() is its decimal.
 struct Panic : std::logic_error {
     explicit Panic(const std::string &w) : std::logic_error(w) {}
+    explicit Panic(int64_t v) : std::logic_error(std::to_string(v)), has_value(true), value(v) {}
+    bool has_value = false;
+    int64_t value = 0;
 };
+
+// err.Error() of the Go value an Err stands for (reader.go:57-76): the wrapped forms carry the
+// detail (the version, reader.go:303 "%w: %v"; the meta id, :319 "%w: 0x%x").
+inline std::string ErrorText(Err e, int64_t detail = 0) {
+    char buf[32];
+    if (e == Err::UnsupportedVersion) {
+        snprintf(buf, sizeof buf, ": %lld", (long long)detail);
+        return std::string(ez_strerror((int)e)) + buf;
+    }
+    if (e == Err::UnsupportedMeta) {
+        snprintf(buf, sizeof buf, ": 0x%llx", (long long)detail);
+        return std::string(ez_strerror((int)e)) + buf;
+    }
+    return ez_strerror((int)e);
+}
 
 // io.Writer: returns bytes taken and an error (Err::OK on success).
 struct IoWriter {
@@ -111,26 +132,33 @@ struct Buffer : IoWriter, IoReader {
 };
 
 namespace detail {
-inline void panic_if(int st, const char *what) {
-    if (st == EZ_EINVAL) throw Panic(what);
+inline void panic_if(int st, int panic) {
+    if (st == EZ_EINVAL) throw Panic(ez_panic_message(panic));
+}
+inline void size_panic(int64_t block, int64_t htable) {  // Writer.init writer.go:161-169
+    const int p = ez_writer_size_panic(block, htable);
+    if (p != EZ_PANIC_NONE) throw Panic(ez_panic_message(p));
 }
 }  // namespace detail
 
 // ---------------------------------------------------------------- codec
 struct Encoder {  // writer.go:537-621
     int Ver = 0;
-    void Tag(std::vector<uint8_t> &b, int tag, int64_t l) const { app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_tag(d, c, n, tag, l); }, "Tag"); }
-    void Offset(std::vector<uint8_t> &b, int64_t off, int64_t l) const { app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_offset(d, c, n, off, l); }, "Offset"); }
-    void MetaTag(std::vector<uint8_t> &b, int64_t meta, int64_t l) const { app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_meta(d, c, n, meta, l); }, "Meta"); }
+    void Tag(std::vector<uint8_t> &b, int tag, int64_t l) const { app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_tag(d, c, n, tag, l); }, EZ_PANIC_LENGTH); }
+    void Offset(std::vector<uint8_t> &b, int64_t off, int64_t l) const { app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_offset(d, c, n, off, l); }, EZ_PANIC_OFFSET); }
+    void MetaTag(std::vector<uint8_t> &b, int64_t meta, int64_t l) const {
+        if (meta & ~(int64_t)MetaTagMask) throw Panic(meta);  // panic(meta) writer.go:600-602
+        app(b, [&](uint8_t *d, size_t c, size_t *n) { return ez_encode_meta(d, c, n, meta, l); }, EZ_PANIC_OFFSET);
+    }
 
   private:
     template <class F>
-    static void app(std::vector<uint8_t> &b, F f, const char *what) {
+    static void app(std::vector<uint8_t> &b, F f, int panic) {
         const size_t at = b.size();
         b.resize(at + 16);
         size_t n = at;
         const int st = f(b.data(), b.size(), &n);
-        detail::panic_if(st, what);
+        detail::panic_if(st, panic);
         b.resize(n);
     }
 };
@@ -157,8 +185,8 @@ class Writer {
     int Ver = 0;              // w.e.Ver
 
     Writer(IoWriter *w, int64_t block, int64_t htable, int device = 0) : W(w) {
+        detail::size_panic(block, htable);
         const int st = ez_writer_new(block, htable, device, &h_);
-        detail::panic_if(st, "eazy: NewWriter: bad block or htable size");
         if (st != EZ_OK) throw std::runtime_error(std::string("eazy: NewWriter: ") + ez_strerror(st));
     }
     ~Writer() { ez_writer_free(h_); }
@@ -172,9 +200,12 @@ class Writer {
         const size_t at = b_.size();
         b_.resize(at + ez_compress_bound(n));
         const int st = ez_writer_write(h_, p, n, b_.data() + at, b_.size() - at, &got);
-        detail::panic_if(st, "eazy: Write");
         b_.resize(at + (st == EZ_OK ? got : 0));
-        if (st != EZ_OK) return {0, (Err)st};
+        if (st != EZ_OK) {
+            failed();  // the handle restarted its stream: so does the mirror
+            detail::panic_if(st, ez_writer_last_panic(h_));
+            return {0, (Err)st};
+        }
         const Err e = write();
         if (e != Err::OK) return {0, e};
         return {n, Err::OK};
@@ -195,8 +226,11 @@ class Writer {
         std::vector<uint8_t> tmp(cap ? cap : 1);
         std::vector<uint64_t> oe(k);
         const int st = ez_writer_write_batch(h_, p, ends, k, tmp.data(), cap, oe.data());
-        detail::panic_if(st, "eazy: WriteBatch");
-        if (st != EZ_OK) return {0, (Err)st};
+        if (st != EZ_OK) {
+            failed();
+            detail::panic_if(st, ez_writer_last_panic(h_));
+            return {0, (Err)st};
+        }
         const uint64_t gen = resets_;
         for (size_t j = 0, prev = 0; j < k; prev = oe[j], j++) {
             b_.insert(b_.end(), tmp.begin() + (ptrdiff_t)prev, tmp.begin() + (ptrdiff_t)oe[j]);
@@ -225,7 +259,8 @@ class Writer {
     }
     void ResetSize(IoWriter *w, int64_t block, int64_t htable) {  // writer.go:155-159
         W = w;
-        detail::panic_if(ez_writer_reset_size(h_, block, htable), "eazy: ResetSize: bad block or htable size");
+        detail::size_panic(block, htable);
+        ez_writer_reset_size(h_, block, htable);
         b_.clear();
         written_ = 0;
     }
@@ -250,6 +285,12 @@ class Writer {
         b_.resize(at + (st == EZ_OK ? got : 0));
         if (st != EZ_OK) return (Err)st;
         return write();
+    }
+    void failed() {  // a device-side failure: the handle is back at a fresh stream; forget w.b too
+        resets_++;
+        if (!ez_writer_is_reset(h_)) ez_writer_reset(h_);
+        b_.clear();
+        written_ = 0;
     }
     void reset() {  // writer.go:187-200
         resets_++;
@@ -372,7 +413,7 @@ inline std::unique_ptr<Reader> NewReaderBytes(const std::vector<uint8_t> &b, int
 // Write; device pointers, asynchronous on `hip_stream`.  See include/eazy.h.
 inline Err CompressBatch(int64_t block, int64_t htable, bool append_magic, const ez_batch &b, void *hip_stream) {
     const int st = ez_compress_batch(block, htable, append_magic ? 0 : EZ_F_NO_MAGIC, &b, hip_stream);
-    detail::panic_if(st, "eazy: CompressBatch: bad block or htable size");
+    if (st == EZ_EINVAL) detail::size_panic(block, htable);
     return (Err)st;
 }
 inline Err DecompressBatch(int64_t block_size_limit, const ez_batch &b, void *workspace, void *hip_stream) {

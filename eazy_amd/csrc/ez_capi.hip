@@ -131,6 +131,25 @@ extern "C" const char *ez_strerror(int code) {
     }
 }
 
+// the value each reference panic carries (writer.go:163, 167, 309/596, 562, 601)
+extern "C" const char *ez_panic_message(int panic) {
+    switch (panic) {
+    case EZ_PANIC_BLOCK: return "block size must be a power of two (32 < bs < 1<<31)";
+    case EZ_PANIC_HTABLE: return "hash table size must be a power of two (hs >= 4)";
+    case EZ_PANIC_LENGTH: return "too big length";
+    case EZ_PANIC_OFFSET: return "too big offset";
+    case EZ_PANIC_META: return "meta";  // Go panics with the meta value itself (an int)
+    default: return "";
+    }
+}
+
+// Writer.init writer.go:161-169: the block check comes first
+extern "C" int ez_writer_size_panic(int64_t block, int64_t htable) {
+    if (((block - 1) & block) != 0 || block < 32 || block > ((int64_t)1 << 31)) return EZ_PANIC_BLOCK;
+    if (((htable - 1) & htable) != 0 || htable < 4) return EZ_PANIC_HTABLE;
+    return EZ_PANIC_NONE;
+}
+
 extern "C" int ez_abi_version(void) { return EZ_ABI_VERSION; }
 extern "C" int ez_device_count(void) { return device_count(); }
 
@@ -221,6 +240,7 @@ struct ez_writer {
     int ver = 0;
     bool pristine = true;  // isreset(): nothing emitted since the last reset
     int64_t pos = 0;       // w.pos
+    int last_panic = EZ_PANIC_NONE;  // the reference panic behind the last EZ_EINVAL
     // dev: [input | in_off[2] out_off[2] out_size status write_idx[2] | write_end[k] | write_out[k] | output]
     DBuf ring, ht, dev;
     HBuf host;             // the same layout, pinned
@@ -292,6 +312,8 @@ extern "C" int ez_writer_set_version(ez_writer *w, int ver) {
 
 extern "C" int ez_writer_is_reset(const ez_writer *w) { return w->pristine ? 1 : 0; }
 
+extern "C" int ez_writer_last_panic(const ez_writer *w) { return w->last_panic; }
+
 // testing hook: w.pos of a handle, ring and table unchanged (positions past 2^32)
 extern "C" int ez_writer_set_position(ez_writer *w, int64_t pos) {
     if (pos < 0) return EZ_EINVAL;
@@ -353,16 +375,32 @@ int writer_run(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, u
         a.max_writes = k;
         a.write_out = dm + 8 + k;
     }
-    EZ_HIP(ez::launch_compress(a, w->stream));
+    // from the launch on, the device history may already hold p: any failure restarts the stream
+    // (as Go does after a failed sink write, writer.go:391-393), so later Writes stay exact
+    hipError_t he = ez::launch_compress(a, w->stream);
     // status, sizes and output back at once (the bound, not the exact size: small Writes)
-    EZ_HIP(hipMemcpyAsync(H + o_meta, D + o_meta, o_o - o_meta + bound, hipMemcpyDeviceToHost, w->stream));
-    EZ_HIP(hipStreamSynchronize(w->stream));
+    if (he == hipSuccess)
+        he = hipMemcpyAsync(H + o_meta, D + o_meta, o_o - o_meta + bound, hipMemcpyDeviceToHost, w->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(w->stream);
+    if (he != hipSuccess) {
+        (void)writer_zero(w);
+        return EZ_EDEVICE;
+    }
     int st = (int)(int32_t)(m[5] & 0xffffffffu);
     const size_t got = (size_t)m[4];
     if (!st && got > bound) st = EZ_ENOSPC;  // cannot happen (tests/test_bound.py)
     if (st) {
         // the device history already holds p while the stream position does not: start the stream
         // over, as Go does after a failed sink write (writer.go:391-393), so later Writes stay exact
+        if (st == EZ_EINVAL) {
+            // Encoder.Tag panics only for lengths of 2^32 - 8 past its Len4 base (writer.go:558-562),
+            // which needs a Write at least that long; the only other panic is the distance check
+            // (writer.go:308-310)
+            const uint64_t tag_limit = ((uint64_t)1 << 32) - 8 + 65916;
+            w->last_panic = EZ_PANIC_OFFSET;
+            for (size_t j = 0; j < k; j++)
+                if (ends[j] - (j ? ends[j - 1] : 0) >= tag_limit) w->last_panic = EZ_PANIC_LENGTH;
+        }
         const int z = writer_zero(w);
         return z ? z : st;
     }

@@ -27,6 +27,7 @@ func compressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
 // NewWriter(block, htable) receiving the Writes streams[k] in order,
 // FlushThreshold 0) and copies every slot back.  One HIP stream per call.
 func compressStreams(streams [][][]byte, block, htable int) ([][]byte, error) {
+	sizePanic(block, htable) // Writer.init writer.go:161-169, as NewWriter would
 	count := len(streams)
 	if count == 0 {
 		return nil, nil

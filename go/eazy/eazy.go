@@ -59,20 +59,22 @@ const (
 
 const Magic = "eazy"
 
-// Errors (reader.go:57-76).
+// Errors (reader.go:57-76): the reference's values, text included.
 var (
 	ErrBadMagic           = errors.New("bad magic")
-	ErrBlockSizeOverLimit = errors.New("block size is over limit")
+	ErrBlockSizeOverLimit = errors.New("block size is more than the limit")
 	ErrNoMagic            = errors.New("no magic")
 	ErrOverflow           = errors.New("length/offset overflow")
 	ErrShortBuffer        = io.ErrShortBuffer
-	ErrUnsupportedMeta    = errors.New("unsupported meta")
-	ErrUnsupportedVersion = errors.New("unsupported version")
-	ErrBreak              = errors.New("break")
-	errMissedMeta         = errors.New("missed meta")
+	ErrUnsupportedMeta    = errors.New("unsupported meta tag")
+	ErrUnsupportedVersion = errors.New("unsupported file format version")
+	ErrBreak              = errors.New("break point")
 	ErrDevice             = errors.New("eazy: no usable MI355X")
 )
 
+// toErr maps a C-ABI status to the Go value the reference returns.  detail is
+// the version (EZ_EUNSUPVER) or the meta id (EZ_EUNSUPMETA).  EZ_EINVAL is
+// a reference panic; panicValue gives its value (callers know which it is).
 func toErr(st C.int, detail int64) error {
 	switch st {
 	case C.EZ_OK:
@@ -92,19 +94,35 @@ func toErr(st C.int, detail int64) error {
 	case C.EZ_EBLOCKLIMIT:
 		return ErrBlockSizeOverLimit
 	case C.EZ_EUNSUPMETA:
-		return fmt.Errorf("meta: %x: %w", detail, ErrUnsupportedMeta) // reader.go:319
+		return fmt.Errorf("%w: 0x%x", ErrUnsupportedMeta, detail) // reader.go:319
 	case C.EZ_EUNSUPVER:
-		return fmt.Errorf("%w: %d", ErrUnsupportedVersion, detail) // reader.go:303
+		return fmt.Errorf("%w: %v", ErrUnsupportedVersion, int(detail)) // reader.go:303
 	case C.EZ_EBREAK:
 		return ErrBreak
 	case C.EZ_EMISSEDMETA:
-		return errMissedMeta
+		return errors.New("missed meta") // reader.go:155: a fresh value each time, as in Go
 	case C.EZ_EINVAL:
-		panic("eazy: invalid argument") // where the reference panics
+		panic(panicValue(C.EZ_PANIC_OFFSET, 0))
 	case C.EZ_EDEVICE:
 		return ErrDevice
 	}
 	return fmt.Errorf("eazy: %s", C.GoString(C.ez_strerror(st)))
+}
+
+// panicValue is the value the reference panics with (writer.go:163, 167, 309,
+// 562, 596): a string, or for Encoder.Meta the meta int itself (:601).
+func panicValue(p C.int, meta int) interface{} {
+	if p == C.EZ_PANIC_META {
+		return meta
+	}
+	return C.GoString(C.ez_panic_message(p))
+}
+
+// sizePanic panics as Writer.init does on invalid sizes (writer.go:161-169).
+func sizePanic(block, htable int) {
+	if p := C.ez_writer_size_panic(C.int64_t(block), C.int64_t(htable)); p != C.EZ_PANIC_NONE {
+		panic(panicValue(p, 0))
+	}
 }
 
 func ptr(b []byte) *C.uint8_t {
@@ -135,11 +153,9 @@ type Writer struct {
 // NewWriter creates a new Writer (writer.go:133-145).  block and htable are
 // powers of two; block is the window size, htable the hash table entries.
 func NewWriter(wr io.Writer, block, htable int) *Writer {
+	sizePanic(block, htable)
 	w := &Writer{Writer: wr, AppendMagic: true}
 	if st := C.ez_writer_new(C.int64_t(block), C.int64_t(htable), 0, &w.h); st != C.EZ_OK {
-		if st == C.EZ_EINVAL {
-			panic("block or htable is not a power of two or too small")
-		}
 		panic(toErr(st, 0))
 	}
 	return w
@@ -171,7 +187,7 @@ func (w *Writer) Write(p []byte) (int, error) {
 	var n C.size_t
 	st := C.ez_writer_write(w.h, ptr(p), C.size_t(len(p)), ptr(out), C.size_t(need), &n)
 	if st != C.EZ_OK {
-		return 0, toErr(st, 0)
+		return 0, w.failed(st)
 	}
 	w.b = w.b[:at+int(n)]
 	if err := w.write(); err != nil {
@@ -218,14 +234,30 @@ func (w *Writer) Reset(wr io.Writer) { w.Writer = wr; w.reset() }
 // ResetSize restarts the stream with new sizes (writer.go:155-159).
 func (w *Writer) ResetSize(wr io.Writer, block, htable int) {
 	w.Writer = wr
+	sizePanic(block, htable)
 	if st := C.ez_writer_reset_size(w.h, C.int64_t(block), C.int64_t(htable)); st != C.EZ_OK {
-		panic("block or htable is not a power of two or too small")
+		panic(toErr(st, 0))
 	}
 	w.b = w.b[:0]
 	w.written = 0
 }
 
 func (w *Writer) reset() { w.resets++; C.ez_writer_reset(w.h); w.b = w.b[:0]; w.written = 0 }
+
+// failed: a device-side failure restarted the handle's stream; the mirror forgets w.b and
+// written with it, and an EZ_EINVAL re-panics with the reference's value.
+func (w *Writer) failed(st C.int) error {
+	w.resets++
+	if C.ez_writer_is_reset(w.h) == 0 {
+		C.ez_writer_reset(w.h)
+	}
+	w.b = w.b[:0]
+	w.written = 0
+	if st == C.EZ_EINVAL {
+		panic(panicValue(C.ez_writer_last_panic(w.h), 0))
+	}
+	return toErr(st, 0)
+}
 
 // WriteBatch compresses several Writes in one device call (no reference counterpart): the sink
 // sees what calling Write on each in turn gives it -- the handle reports where each Write's
@@ -249,7 +281,7 @@ func (w *Writer) WriteBatch(ps [][]byte) (int, error) {
 	st := C.ez_writer_write_batch(w.h, ptr(data), (*C.uint64_t)(unsafe.Pointer(&ends[0])), C.size_t(len(ps)),
 		ptr(out), C.size_t(need), (*C.uint64_t)(unsafe.Pointer(&oe[0])))
 	if st != C.EZ_OK {
-		return 0, toErr(st, 0)
+		return 0, w.failed(st)
 	}
 	gen, prev, done := w.resets, uint64(0), 0
 	for j := range ps {

@@ -54,3 +54,36 @@ func TestCompressBatch(t *testing.T) {
 		}
 	}
 }
+
+// The reference's error and panic values, text included (reader.go:57-76, 303, 319;
+// writer.go:163, 167, 562, 596, 601).
+func TestErrorText(t *testing.T) {
+	for _, c := range []struct {
+		err  error
+		want string
+	}{
+		{ErrBlockSizeOverLimit, "block size is more than the limit"},
+		{ErrUnsupportedMeta, "unsupported meta tag"},
+		{ErrUnsupportedVersion, "unsupported file format version"},
+		{ErrBreak, "break point"},
+		{toErr(C_EUNSUPMETA, 0x28), "unsupported meta tag: 0x28"},
+		{toErr(C_EUNSUPVER, 1), "unsupported file format version: 1"},
+	} {
+		if c.err.Error() != c.want {
+			t.Errorf("%q, want %q", c.err.Error(), c.want)
+		}
+	}
+	expectPanic := func(want interface{}, f func()) {
+		defer func() {
+			if r := recover(); r != want {
+				t.Errorf("panic %v, want %v", r, want)
+			}
+		}()
+		f()
+	}
+	expectPanic("block size must be a power of two (32 < bs < 1<<31)", func() { NewWriter(nil, 31, 16) })
+	expectPanic("hash table size must be a power of two (hs >= 4)", func() { NewWriter(nil, 1024, 3) })
+	expectPanic("too big length", func() { Encoder{}.Tag(nil, Literal, 0x1_1000_0000) })
+	expectPanic("too big offset", func() { Encoder{}.Offset(nil, 0x1_1000_0000, 10) })
+	expectPanic(1024, func() { Encoder{}.Meta(nil, 1024, 4) })
+}

@@ -66,6 +66,22 @@ enum {
 #define EZ_VERSION 0
 
 const char *ez_strerror(int code);
+
+/* ---- which reference panic an EZ_EINVAL stands for, so a shim re-panics with Go's value ----
+ * ez_encode_tag: always EZ_PANIC_LENGTH (writer.go:562); ez_encode_offset: EZ_PANIC_OFFSET
+ * (:596); ez_encode_meta: EZ_PANIC_META when meta & ~0xf8 (:600-602, Go panics with the meta
+ * int), else EZ_PANIC_OFFSET (its wide length goes through Offset); a Writer handle:
+ * ez_writer_last_panic; NewWriter / ResetSize: ez_writer_size_panic. */
+enum {
+    EZ_PANIC_NONE = 0,
+    EZ_PANIC_BLOCK = 1,  /* "block size must be a power of two (32 < bs < 1<<31)" writer.go:163 */
+    EZ_PANIC_HTABLE = 2, /* "hash table size must be a power of two (hs >= 4)"    writer.go:167 */
+    EZ_PANIC_LENGTH = 3, /* "too big length"                                       writer.go:562 */
+    EZ_PANIC_OFFSET = 4, /* "too big offset"                                       writer.go:309, 596 */
+    EZ_PANIC_META = 5    /* panic(meta)                                            writer.go:601 */
+};
+const char *ez_panic_message(int panic);
+int ez_writer_size_panic(int64_t block, int64_t htable); /* Writer.init writer.go:161-169; 0 = valid */
 int ez_abi_version(void);
 /* Number of visible HIP devices (0 when none). */
 int ez_device_count(void);
@@ -112,6 +128,7 @@ int ez_writer_break(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n);  /* 
 int ez_writer_reset(ez_writer *w);                                          /* Reset       writer.go:149 (reset :187) */
 int ez_writer_reset_size(ez_writer *w, int64_t block, int64_t htable);     /* ResetSize   writer.go:155 */
 int ez_writer_is_reset(const ez_writer *w);                                 /* isreset     writer.go:403 */
+int ez_writer_last_panic(const ez_writer *w); /* EZ_PANIC_* behind the handle's last EZ_EINVAL */
 /* Testing hook (no reference counterpart): set w.pos, ring and table unchanged, so a test can
  * run Writes across stream position 2^32, where the table's uint32 values (writer.go:216-217)
  * stop matching; the C oracle has the same hook. */

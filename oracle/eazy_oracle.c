@@ -858,7 +858,7 @@ typedef struct {
     int64_t block, htable;
     const uint8_t *in;
     const int64_t *in_off, *in_sizes;
-    int64_t count, next;
+    int64_t count, next, grain;
     uint8_t *out;
     const int64_t *out_off;
     int64_t *sizes;
@@ -873,10 +873,10 @@ static void *batch_worker(void *arg) {
     for (;;) {
         pthread_mutex_lock(&j->mu);
         int64_t s0 = j->next;
-        j->next += 64;
+        j->next += j->grain;
         pthread_mutex_unlock(&j->mu);
         if (s0 >= j->count) break;
-        int64_t s1 = s0 + 64 < j->count ? s0 + 64 : j->count;
+        int64_t s1 = s0 + j->grain < j->count ? s0 + j->grain : j->count;
         for (int64_t s = s0; s < s1; s++) {
             int e;
             if (j->kind == 0) {
@@ -905,6 +905,11 @@ static void *batch_worker(void *arg) {
 
 static int run_batch(batch_job *j, int nthreads) {
     if (nthreads < 1) nthreads = 1;
+    /* streams handed out in grains of at most 64, and small enough that every
+       thread gets work (a batch of 64 long streams spreads over all threads) */
+    j->grain = j->count / ((int64_t)nthreads * 4);
+    if (j->grain > 64) j->grain = 64;
+    if (j->grain < 1) j->grain = 1;
     pthread_mutex_init(&j->mu, NULL);
     pthread_t *t = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
     for (int k = 0; k < nthreads; k++) pthread_create(&t[k], NULL, batch_worker, j);

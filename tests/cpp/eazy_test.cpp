@@ -144,11 +144,44 @@ static void TestReaderShortBuffer() {  // eazy_test.go:858-978
 static void TestEncoderPanics() {  // eazy_test.go:895, 946, TestMeta :814
     Encoder e;
     Bytes b;
-    bool p1 = false, p2 = false, p3 = false;
-    try { e.Tag(b, Literal, 0x110000000LL); } catch (const Panic &) { p1 = true; }
-    try { e.Offset(b, 0x110000000LL, 10); } catch (const Panic &) { p2 = true; }
-    try { e.MetaTag(b, 1024, 4); } catch (const Panic &) { p3 = true; }
-    CHECK(p1 && p2 && p3);
+    bool p1 = false, p2 = false, p3 = false, p4 = false;
+    // the panic values themselves (writer.go:562, 596, 601)
+    try { e.Tag(b, Literal, 0x110000000LL); } catch (const Panic &p) { p1 = std::string(p.what()) == "too big length"; }
+    try { e.Offset(b, 0x110000000LL, 10); } catch (const Panic &p) { p2 = std::string(p.what()) == "too big offset"; }
+    try { e.MetaTag(b, 1024, 4); } catch (const Panic &p) { p3 = p.has_value && p.value == 1024; }
+    try { e.MetaTag(b, MetaReset, 0x110000000LL); } catch (const Panic &p) { p4 = std::string(p.what()) == "too big offset"; }
+    CHECK(p1 && p2 && p3 && p4);
+}
+
+static std::string size_panic(int64_t bs, int64_t hs) {
+    try {
+        Buffer buf;
+        NewWriter(&buf, bs, hs);
+    } catch (const Panic &p) {
+        return p.what();
+    } catch (...) {
+        return "(no panic)";
+    }
+    return "(no panic)";
+}
+
+static void TestErrorText() {  // reader.go:57-76, 303, 319; Writer.init writer.go:161-169
+    CHECK(ErrorText(Err::BadMagic) == "bad magic");
+    CHECK(ErrorText(Err::BlockSizeOverLimit) == "block size is more than the limit");
+    CHECK(ErrorText(Err::NoMagic) == "no magic");
+    CHECK(ErrorText(Err::Overflow) == "length/offset overflow");
+    CHECK(ErrorText(Err::ShortBuffer) == "short buffer");
+    CHECK(ErrorText(Err::UnsupportedMeta, 0x28) == "unsupported meta tag: 0x28");
+    CHECK(ErrorText(Err::UnsupportedVersion, 1) == "unsupported file format version: 1");
+    CHECK(ErrorText(Err::Break) == "break point");
+    CHECK(ErrorText(Err::MissedMeta) == "missed meta");
+    CHECK(ErrorText(Err::EOF_) == "EOF");
+    CHECK(ErrorText(Err::UnexpectedEOF) == "unexpected EOF");
+    const std::string bsp = "block size must be a power of two (32 < bs < 1<<31)";
+    const std::string hsp = "hash table size must be a power of two (hs >= 4)";
+    CHECK(size_panic(31, 16) == bsp && size_panic(16, 16) == bsp && size_panic(1LL << 32, 16) == bsp);
+    CHECK(size_panic(48, 3) == bsp);  // the block check comes first
+    CHECK(size_panic(1024, 3) == hsp && size_panic(1024, 6) == hsp && size_panic(1024, 0) == hsp);
 }
 
 static void TestCompressBound() {  // include/eazy.h, tests/test_bound.py
@@ -331,6 +364,7 @@ static void TestUnsupportedVersion() {  // eazy_test.go:749-762
     auto r = NewReaderBytes(buf.b);
     auto [got, err] = rd(*r, 1);
     CHECK(err == Err::UnsupportedVersion && got.empty());
+    CHECK(ErrorText(err, r->Detail) == "unsupported file format version: 1");
 }
 
 struct FailingSink : IoWriter {  // accepts `accept` bytes once, then fails
@@ -446,6 +480,7 @@ int main(int argc, char **argv) {
     run("TestPrintOffsetEncoding", TestPrintOffsetEncoding);
     run("TestReaderShortBuffer", TestReaderShortBuffer);
     run("TestEncoderPanics", TestEncoderPanics);
+    run("TestErrorText", TestErrorText);
     run("TestCompressBound", TestCompressBound);
     if (!cpu) {
         if (ez_device_count() <= 0) {

@@ -24,10 +24,10 @@ def _run(*args):
 
 def test_cpp_host_only():
     out = _run("--cpu")
-    assert "5/5 passed" in out
+    assert "6/6 passed" in out
 
 
 @pytest.mark.gpu
 def test_cpp_full(cuda):
     out = _run()
-    assert "FAIL" not in out and "21/21 passed" in out
+    assert "FAIL" not in out and "22/22 passed" in out

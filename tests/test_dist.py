@@ -71,6 +71,35 @@ def test_two_rank_gloo_exchange(tmp_path):
     _run(tmp_path, "cpu")
 
 
+def test_bench_launches_ranks_itself():
+    """`python bench.py --gpus 2` outside torchrun starts the 2 ranks itself (one
+    child process tree) and rank 0's JSON line comes back on stdout; the
+    rehearsal runs the same shard split, size all-gather and payload gather."""
+    import json
+
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    bench = os.path.join(os.path.dirname(HERE), "bench.py")
+    p = subprocess.run([sys.executable, bench, "--gpus", "2", "--rehearse", "--streams", "67", "--stream-bytes", "300"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["streams_per_rank"] == [33, 34] and res["gathered_equals_input"]
+    assert res["bytes_gathered"] == 67 * 300
+
+
+def test_bench_rejects_world_mismatch():
+    """--gpus must equal the world size the launch ends up with."""
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    bench = os.path.join(os.path.dirname(HERE), "bench.py")
+    p = subprocess.run([sys.executable, bench, "--gpus", "2", "--rehearse"], env=env, capture_output=True, text=True,
+                       timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
 @pytest.mark.gpu
 def test_two_rank_exchange_gpu_kernels(tmp_path, cuda):
     _run(tmp_path, "gpu")
