@@ -58,7 +58,20 @@ class DeviceError(EazyError):
 
 
 class Panic(EazyError):
-    """Where the reference panics (bad sizes, too big length/offset, bad meta)."""
+    """Where the reference panics (bad sizes, too big length/offset, bad meta); str() is
+    the reference's panic value when known (writer.go:163, 167, 309, 562, 596)."""
+
+    def __init__(self, code: int = 12, detail: int = 0, message: str | None = None):
+        super().__init__(code, detail)
+        if message is not None:
+            self.args = (message,)
+
+
+def _size_panic(block: int, htable: int) -> None:
+    """Writer.init writer.go:161-169: the reference's panic for invalid sizes."""
+    p = _lib().ez_writer_size_panic(block, htable)
+    if p:
+        raise Panic(12, message=_lib().ez_panic_message(p).decode())
 
 
 def _strerror(code: int) -> str:
@@ -100,6 +113,10 @@ def _lib():
     L.ez_writer_reset.argtypes = [vp]
     L.ez_writer_reset_size.argtypes = [vp, i64, i64]
     L.ez_writer_is_reset.argtypes = [vp]
+    L.ez_writer_last_panic.argtypes = [vp]
+    L.ez_writer_size_panic.argtypes = [i64, i64]
+    L.ez_panic_message.restype = C.c_char_p
+    L.ez_panic_message.argtypes = [C.c_int]
     L.ez_reader_new.argtypes = [C.c_int, C.POINTER(vp)]
     L.ez_reader_free.argtypes = [vp]
     L.ez_reader_configure.argtypes = [vp, i64, C.c_int, C.c_int]
@@ -230,6 +247,7 @@ class Writer:
     """
 
     def __init__(self, wr, block: int, htable: int, device: int = 0):
+        _size_panic(block, htable)
         h = C.c_void_p()
         _check(_lib().ez_writer_new(block, htable, device, C.byref(h)))
         self._h = h
@@ -272,9 +290,25 @@ class Writer:
 
     def Write(self, p: bytes) -> int:  # writer.go:206-337
         p = bytes(p)
-        self._b += self._call(_lib().ez_writer_write, p, len(p), cap=compress_bound(len(p)))
+        try:
+            b = self._call(_lib().ez_writer_write, p, len(p), cap=compress_bound(len(p)))
+        except EazyError as e:
+            raise self._failed(e) from None
+        self._b += b
         self._write()
         return len(p)
+
+    def _failed(self, e: EazyError) -> EazyError:
+        """A device-side failure restarted the handle's stream: the mirror forgets w.b and
+        written too; an EZ_EINVAL carries the reference's panic value."""
+        self._resets += 1
+        if not _lib().ez_writer_is_reset(self._h):
+            _lib().ez_writer_reset(self._h)
+        self._b = bytearray()
+        self._written = 0
+        if isinstance(e, Panic):
+            return Panic(EINVAL, message=_lib().ez_panic_message(_lib().ez_writer_last_panic(self._h)).decode())
+        return e
 
     def WriteBatch(self, ps) -> int:
         """Several Writes in one device call (no reference counterpart; a throughput form of
@@ -296,7 +330,10 @@ class Writer:
         cap = sum(compress_bound(len(p)) for p in ps)
         buf = (C.c_uint8 * max(cap, 1))()
         oe = (C.c_uint64 * k)()
-        _check(_lib().ez_writer_write_batch(self._h, b"".join(ps), ends, k, buf, cap, oe))
+        try:
+            _check(_lib().ez_writer_write_batch(self._h, b"".join(ps), ends, k, buf, cap, oe))
+        except EazyError as e:
+            raise self._failed(e) from None
         out = bytes(buf[: oe[k - 1]])
         prev, gen = 0, self._resets
         for j in range(k):
@@ -329,6 +366,7 @@ class Writer:
 
     def ResetSize(self, wr, block: int, htable: int) -> None:  # writer.go:155-159
         self.Writer = wr
+        _size_panic(block, htable)
         _check(_lib().ez_writer_reset_size(self._h, block, htable))
         self._b = bytearray()
         self._written = 0

@@ -103,7 +103,7 @@ __global__ __launch_bounds__(64) void kx_pred(CompressArgs A, KxBufs B) {
     const int64_t lo = (int64_t)k * kChunk;
     if (lo + 4 > n || (uint64_t)n > A.max_len) return;
     const uint8_t *p = A.in + A.in_off[s];
-    uint16_t *pr = B.pred + (A.in_off[s] - A.in_off[0]);  // offsets are absolute (views of a larger batch)
+    uint16_t *pr = B.pred + s * A.max_len;  // per stream: a refused over-long stream cannot shift the others
     const uint32_t hsh = hshift(A.hs);
     for (int64_t h = lane; h < A.hs; h += 64) T[h] = kNone;
     __syncthreads();
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
         if (xb + 4 > n) continue;  // uniform: the block's values only
         const uint8_t *p = A.in + A.in_off[s];
         // the piece's rows, block-uniform (a piece never straddles a kx_pred chunk: both aligned)
-        const uint16_t *prow = B.pred + (A.in_off[s] - A.in_off[0]);
+        const uint16_t *prow = B.pred + s * A.max_len;
         const uint32_t *trow = B.tabs + (s * B.kmax + (uint64_t)(xb / kChunk)) * (uint64_t)A.hs;
         const uint32_t *srow = A.spec_tab + s * (uint64_t)A.hs;
         // stage bytes [xb - 8, xb + kPiece + 24) by coalesced aligned words (outside the batch: 0);

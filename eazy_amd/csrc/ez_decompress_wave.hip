@@ -364,21 +364,22 @@ __global__ __launch_bounds__(64) void k2_wave(DecompressArgs A) {
         }
 }
 
-// every deferred literal's bytes, 64 KiB per block step
+// every deferred literal's bytes, 64 KiB pieces per block step
 __global__ __launch_bounds__(256) void kd_copy(DecompressArgs A, uint64_t kp) {
     const uint64_t nl = A.defer[0] < A.defer_cap ? A.defer[0] : A.defer_cap;
     const DeferLit *rec = (const DeferLit *)(A.defer + 4);
     const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
     for (uint64_t q = blockIdx.x; q < nl * kp; q += gridDim.x) {
         const DeferLit L = rec[q / kp];
-        const uint64_t b = (q % kp) * 65536;
-        if (b >= L.len) continue;
-        const uint64_t e = b + 65536 < L.len ? b + 65536 : L.len;
-        for (uint64_t k = b + 16 * threadIdx.x; k < e; k += 16 * 256) {
-            const uint8_t *y = A.in + L.src + k;
-            const V16 v = y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
-            if (k + 16 <= e) st16v(A.out + L.dst + k, v);
-            else put_small(A.out + L.dst + k, v, (uint32_t)(e - k));
+        // kp is a hint (the caller's largest slot): a longer literal's block takes every kp-th piece
+        for (uint64_t b = (q % kp) * 65536; b < L.len; b += kp * 65536) {
+            const uint64_t e = b + 65536 < L.len ? b + 65536 : L.len;
+            for (uint64_t k = b + 16 * threadIdx.x; k < e; k += 16 * 256) {
+                const uint8_t *y = A.in + L.src + k;
+                const V16 v = y + 16 <= hi ? ld16v(y) : ld_clamped(y, lo, hi);
+                if (k + 16 <= e) st16v(A.out + L.dst + k, v);
+                else put_small(A.out + L.dst + k, v, (uint32_t)(e - k));
+            }
         }
     }
 }

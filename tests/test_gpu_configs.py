@@ -167,3 +167,70 @@ def test_k2w_deferred_literals(cuda):
         b"".join(R + R[:4]) + R[2][:500],                           # ten long literals: eight deferred
     ]
     _gpu_check(cuda, bufs)
+
+
+@pytest.mark.gpu
+def test_c2_production_routing_k1l_four_per_wave(cuda):
+    """C2's production route: more than 256 fresh 256 KiB log streams go from K1s to K1L
+    at 4 streams per wave (u32 tables, trims, ring image); 260 streams, automatic choice,
+    every stream byte-compared with the oracle and decoded by every K2 decoder."""
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    assert ez.compress_kernel(MiB, 1024, 256 << 10, 260) == "s"
+    d = synth.logs(37, 260 * (256 << 10)).tobytes()
+    _gpu_check(cuda, [d[k << 18 : (k + 1) << 18] for k in range(260)])
+
+
+@pytest.mark.gpu
+def test_k2w_literal_longer_than_the_hint(cuda):
+    """K2w defers literals of 16 KiB and more to kd_copy; the decode's max_len hint (64 KiB
+    here) must not bound how much of a 256 KiB literal gets copied."""
+    import torch
+
+    import eazy_amd as ez
+
+    rng = np.random.default_rng(67)
+    bufs = [rng.integers(0, 256, 256 << 10, dtype=np.uint8).tobytes(), bytes(1000) + rng.integers(0, 256, 200000, dtype=np.uint8).tobytes()]
+    want = [orc.compress(MiB, 1024, [b]) for b in bufs]
+    dev = cuda
+    comp = torch.from_numpy(np.frombuffer(b"".join(want) + bytes(64), np.uint8).copy()).to(dev)
+    coff = torch.tensor([0, len(want[0]), len(want[0]) + len(want[1])], dtype=torch.int64, device=dev)
+    ooff = torch.tensor([0, len(bufs[0]), len(bufs[0]) + len(bufs[1])], dtype=torch.int64, device=dev)
+    ez.select_decompress_kernel("w")
+    try:
+        out, sz, st = ez.decompress_batch(comp, coff, ooff, max_len=64 << 10)
+    finally:
+        ez.select_decompress_kernel("")
+    assert st.cpu().tolist() == [0, 0] and sz.cpu().tolist() == [len(b) for b in bufs]
+    assert out[: len(bufs[0]) + len(bufs[1])].cpu().numpy().tobytes() == b"".join(bufs)
+
+
+@pytest.mark.gpu
+def test_k1x_refused_stream_leaves_others_exact(cuda):
+    """A stream longer than the caller's max_len is refused (EINVAL); K1x's per-position
+    scratch is indexed per stream, so the refused stream cannot shift or overwrite the
+    others' tables: they stay oracle-exact."""
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    d = synth.logs(41, 700 << 10).tobytes()
+    bufs = [d[: 300 << 10]] + [d[(300 + 100 * k) << 10 : (400 + 100 * k) << 10] for k in range(4)]
+    lens = np.array([len(b) for b in bufs], np.int64)
+    offs = torch.from_numpy(np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)).to(cuda)
+    data = torch.from_numpy(np.frombuffer(b"".join(bufs), np.uint8).copy()).to(cuda)
+    for kind in ("x", ""):
+        ez.select_compress_kernel(kind)
+        try:
+            cb = ez.compress_batch(data, offs, MiB, 1024, max_len=128 << 10)
+        finally:
+            ez.select_compress_kernel("")
+        st = cb.status.cpu().tolist()
+        assert st[0] == ez.EINVAL and st[1:] == [0, 0, 0, 0], (kind, st)
+        so, sz = cb.slot_off.cpu().numpy(), cb.sizes.cpu().numpy()
+        slots = cb.slots.cpu().numpy()
+        for s in range(1, 5):
+            got = slots[so[s] : so[s] + sz[s]].tobytes()
+            assert got == orc.compress(MiB, 1024, [bufs[s]]), f"K1 {kind!r} stream {s}: bytes differ"
