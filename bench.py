@@ -499,7 +499,6 @@ def main():
     world, rank, local = R.world, R.rank, R.local
     if world > 1:
         dist.init_process_group("nccl")
-    local = local % max(1, torch.cuda.device_count())  # ranks beyond the node's GPUs share (rehearsals on one card)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 

@@ -705,7 +705,7 @@ extern "C" int ez_select_compress_kernel(int kind) {
 }
 
 extern "C" int ez_select_decompress_kernel(int kind) {
-    if (kind != 0 && kind != 'r' && kind != 'w') return EZ_EINVAL;
+    if (kind != 0 && kind != 'r' && kind != 'w' && kind != 't') return EZ_EINVAL;
     ez::select_decompress_variant(kind);
     return EZ_OK;
 }

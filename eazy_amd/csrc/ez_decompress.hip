@@ -267,7 +267,24 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     if (e != hipSuccess) return e;
     if (g_decompress_variant < 0) {
         const char *v = getenv("EZ_K2");
-        g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w' : (v && strcmp(v, "ring") == 0 ? 'r' : 0);
+        g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w' : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : 0));
+    }
+    if (g_decompress_variant == 't') {
+        // K2t: token-parallel, a wave per stream; its hand-overs go to the exact decoder, the long
+        // literals it defers are moved last (the exact decoder writes the same bytes for a stream it takes)
+        DecompressArgs b = a;
+        b.defer = a.slow + 2 * a.count + 32;
+        b.defer_cap = a.count * (uint64_t)kDefSlots;
+        if ((e = hipMemsetAsync(b.defer, 0, 16, st)) != hipSuccess) return e;
+        e = launch_decompress_tok(b, st);
+        if (e != hipSuccess) return e;
+#if (EZ_EXP & 4096)
+        return e;  // debug builds: the hand-over codes stay in the statuses
+#endif
+        const uint64_t grid = a.count < 4096 ? a.count : 4096;
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        return launch_defer_copy(b, st);
     }
     // K2w for long slots, unless the batch holds enough streams for K2r's lane per stream to
     // outrun K2w's wave per stream (1 GiB batches: 16 Ki x 64 KiB 147 vs 101 GiB/s for K2r,

@@ -90,6 +90,28 @@ __host__ __device__ __forceinline__ int k2_scan(V16 h, int32_t i, int32_t nb, in
     return kParseToken;
 }
 
+// The common token forms from the header's first 8 bytes, in 32-bit arithmetic without
+// branches: a 1-byte tag (length 1..123; not padding, not a meta) and, for a copy, a 1..3-byte
+// offset (plain, Off1 or Off2, reader.go:422-472) after an optional long prefix (:394-420).
+// Returns a value < 0 for another form (k2_parse decides); D is the copy distance, adv the
+// input bytes taken.  (Conditions as sign bits of one integer: compares would each become a
+// lane mask and every && a scalar instruction.)
+__host__ __device__ __forceinline__ int32_t fast_tok(uint64_t lo, int32_t &L, int32_t &adv, uint32_t &D, bool &cp) {
+    const uint32_t w0 = (uint32_t)lo;
+    const uint32_t l7 = w0 & 0x7f;
+    cp = (w0 & 0x80) != 0;
+    L = (int32_t)l7;
+    const bool lng = (w0 & 0xff00) == 0xff00;
+    const uint32_t y = (uint32_t)(lo >> (lng ? 16 : 8));  // the offset's bytes
+    const uint32_t o = y & 0xff;
+    const bool w = o >= 252, w2 = o == 253;
+    const uint32_t ext = w2 ? 256 + ((y >> 8) & 0xffff) : (y >> 8) & 0xff;
+    const uint32_t D0 = w ? 252 + ext : o;
+    D = lng ? D0 : D0 + l7;
+    adv = cp ? 2 + (int32_t)lng + (int32_t)w + (int32_t)w2 : 1 + L;
+    return (L - 1) | (122 - (L - 1)) | (cp ? 253 - (int32_t)o : 0);
+}
+
 // the checks on the decoder's state: output position pos in a slot of cap bytes and
 // bsl = log2 of the window after MetaReset (-1: none yet; updated here)
 __host__ __device__ __forceinline__ int k2_check(int r, const K2Tok &t, int32_t pos, int32_t cap, int32_t &bsl) {

@@ -197,13 +197,14 @@ def test_k2w_literal_longer_than_the_hint(cuda):
     comp = torch.from_numpy(np.frombuffer(b"".join(want) + bytes(64), np.uint8).copy()).to(dev)
     coff = torch.tensor([0, len(want[0]), len(want[0]) + len(want[1])], dtype=torch.int64, device=dev)
     ooff = torch.tensor([0, len(bufs[0]), len(bufs[0]) + len(bufs[1])], dtype=torch.int64, device=dev)
-    ez.select_decompress_kernel("w")
-    try:
-        out, sz, st = ez.decompress_batch(comp, coff, ooff, max_len=64 << 10)
-    finally:
-        ez.select_decompress_kernel("")
-    assert st.cpu().tolist() == [0, 0] and sz.cpu().tolist() == [len(b) for b in bufs]
-    assert out[: len(bufs[0]) + len(bufs[1])].cpu().numpy().tobytes() == b"".join(bufs)
+    for kind in ("w", "t"):
+        ez.select_decompress_kernel(kind)
+        try:
+            out, sz, st = ez.decompress_batch(comp, coff, ooff, max_len=64 << 10)
+        finally:
+            ez.select_decompress_kernel("")
+        assert st.cpu().tolist() == [0, 0] and sz.cpu().tolist() == [len(b) for b in bufs], kind
+        assert out[: len(bufs[0]) + len(bufs[1])].cpu().numpy().tobytes() == b"".join(bufs), kind
 
 
 @pytest.mark.gpu

@@ -89,4 +89,4 @@ def test_oracle_batch_spreads_few_streams_over_threads():
         res[n] = orc.compress_batch(1 << 20, 1024, data, offs, slot, n)
         t[n] = time.perf_counter() - t0
     assert np.array_equal(res[1][1], res[threads][1]) and np.array_equal(res[1][0], res[threads][0])
-    assert t[1] / t[threads] > threads / 3, f"{threads} threads only {t[1] / t[threads]:.2f}x faster than one"
+    assert t[1] / t[threads] > 2, f"{threads} threads only {t[1] / t[threads]:.2f}x faster than one"
