@@ -151,6 +151,16 @@ extern "C" int ez_writer_size_panic(int64_t block, int64_t htable) {
 }
 
 extern "C" int ez_abi_version(void) { return EZ_ABI_VERSION; }
+
+#ifdef EZ_KNOBS
+namespace ez {
+const char *knob_str(const char *name) { return getenv(name); }
+int knob(const char *name, int dflt) {
+    const char *v = getenv(name);
+    return v ? atoi(v) : dflt;
+}
+}  // namespace ez
+#endif
 extern "C" int ez_device_count(void) { return device_count(); }
 
 // ------------------------------------------------------------------ token codec

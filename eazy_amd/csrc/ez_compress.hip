@@ -714,7 +714,7 @@ void select_compress_variant(int v) { g_forced_variant = v; }
 char compress_variant(const CompressArgs &a) {
     int &forced = g_forced_variant;
     if (forced < 0) {
-        const char *e = getenv("EZ_K1");
+        const char *e = knob_str("EZ_K1");
         forced = e && std::string(e) == "general" ? 'w' : (e && std::string(e) == "long" ? 'l' : 0);
     }
     if (forced == 'w') return 'w';
@@ -744,7 +744,7 @@ hipError_t launch_general(const CompressArgs &a, hipStream_t st) {
     CompressArgs b = a;
     b.win_bytes = 0;
     if (!ring && !pl && !a.write_idx && a.max_len > (uint64_t)kPLdsMax) {  // long streams: the LDS window
-        static const uint32_t w = getenv("EZ_K1W_WIN") ? (uint32_t)atoi(getenv("EZ_K1W_WIN")) & ~15u : kWinBytes;
+        static const uint32_t w = (uint32_t)knob("EZ_K1W_WIN", (int)kWinBytes) & ~15u;
         b.win_bytes = w;
         if (w) lds += w + 32;
     }

@@ -358,8 +358,7 @@ __global__ __launch_bounds__(256) void kx_copy(CompressArgs A, KxBufs B) {
 
 int rounds() {
     static const int r = [] {
-        const char *e = getenv("EZ_K1X_ROUNDS");
-        const int v = e ? atoi(e) : kRounds;
+        const int v = knob("EZ_K1X_ROUNDS", kRounds);
         return v >= 0 && v <= 1024 ? v : kRounds;
     }();
     return r;
@@ -393,7 +392,7 @@ Layout layout(const CompressArgs &a) {
 // kernel's chain is short), their positions and outputs fit u32 and the table fits LDS; the
 // scratch (u16 per input byte, one table per chunk) stays bounded.
 bool spec_applies(const CompressArgs &a, bool any_len) {
-    static const bool off = getenv("EZ_K1X") && atoi(getenv("EZ_K1X")) == 0;  // A/B: the general kernel alone
+    static const bool off = knob("EZ_K1X", 1) == 0;  // A/B: the general kernel alone
     if (off || a.max_len == 0 || a.ring || a.write_idx || a.start != 0 || !a.header || a.hs > 4096 || (a.max_len < (64u << 10) && !any_len) ||
         a.max_len >= (1ull << 31) || a.count == 0)
         return false;
@@ -452,7 +451,7 @@ hipError_t launch_compress_spec(const CompressArgs &a0, uint8_t *scratch, hipStr
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(kx_copy, dim3(jgrid), dim3(256), 0, st, a, B);
     if (!check()) return e;
-    if (getenv("EZ_K1X_DEBUG")) {  // diagnostics: streams left to the general kernel's serial continuation
+    if (knob_str("EZ_K1X_DEBUG")) {  // diagnostics: streams left to the general kernel's serial continuation
         std::vector<SpecState> h(a.count);
         uint32_t nl[2];
         (void)hipStreamSynchronize(st);

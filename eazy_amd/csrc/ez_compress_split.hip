@@ -1297,13 +1297,13 @@ uint32_t split_stride(const CompressArgs &a) {
 // lanes per stream for T32: 32 when the batch has few streams (long Writes, C2: two
 // waves per SIMD instead of one, 33.3 vs 34.3 ms); EZ_K1S_G32=16|32 overrides
 int split_g32(uint64_t count) {
-    static const int g = getenv("EZ_K1S_G32") ? atoi(getenv("EZ_K1S_G32")) : 0;
+    static const int g = knob("EZ_K1S_G32", 0);
     if (g == 32 || g == 16) return g;
     return count <= 8192 ? 32 : 16;
 }
 bool g_split_t32 = false;  // ez_select_compress_kernel('S')
 bool split_t32_forced() {
-    static const bool v = getenv("EZ_K1S_T") && atoi(getenv("EZ_K1S_T")) == 32;
+    static const bool v = knob("EZ_K1S_T", 0) == 32;
     return v || g_split_t32;
 }
 
@@ -1319,11 +1319,11 @@ hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st)
     const uint64_t rcap = rec_cap(a);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
-    static const size_t pad = getenv("EZ_K1S_LDSPAD") ? (size_t)atoi(getenv("EZ_K1S_LDSPAD")) : 0;
+    static const size_t pad = (size_t)knob("EZ_K1S_LDSPAD", 0);
     // wave priority (s_setprio 3) on the chain up to the candidate loads' issue: bit 0 (default),
     // bit 1 around the next window's load; EZ_K1S_PRIO=0|1|2|3 (A/B, same box: 3.58 / 3.52 /
     // 3.58 / 3.53 ms at C1)
-    static const int prio = getenv("EZ_K1S_PRIO") ? atoi(getenv("EZ_K1S_PRIO")) : 1;
+    static const int prio = knob("EZ_K1S_PRIO", 1);
     hipLaunchKernelGGL((k1_parse<G, T16, MW>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap,
                        prio);
     hipError_t e = hipGetLastError();
@@ -1335,7 +1335,7 @@ hipError_t launch_split_g(const CompressArgs &a, uint64_t *recs, hipStream_t st)
 
 // the lean single-Write parse (k1_lean) + the token writer; EZ_K1S_LEAN=0 takes k1_parse (A/B)
 bool split_lean() {
-    static const bool v = !(getenv("EZ_K1S_LEAN") && atoi(getenv("EZ_K1S_LEAN")) == 0);
+    static const bool v = knob("EZ_K1S_LEAN", 1) != 0;
     return v;
 }
 hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
@@ -1348,13 +1348,13 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     const uint32_t stride = split_stride<16, true>(a), tw = split_table_words<true>(a);
     const uint64_t rcap = rec_cap(a);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
-    static const int prio = getenv("EZ_K1S_PRIO") ? atoi(getenv("EZ_K1S_PRIO")) : 1;
+    static const int prio = knob("EZ_K1S_PRIO", 1);
     uint8_t *edge = (uint8_t *)(recs + a.count * rcap);
     hipError_t z = hipMemsetAsync(edge, 0, 128, st);
     if (z == hipSuccess) z = hipMemsetAsync(edge + 128 + kEdgeSlots * edge_slot_bytes(a), 0, 16, st);
     if (z != hipSuccess) return z;
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
-    static const size_t pad = getenv("EZ_K1S_LDSPAD") ? (size_t)atoi(getenv("EZ_K1S_LDSPAD")) : 0;
+    static const size_t pad = (size_t)knob("EZ_K1S_LDSPAD", 0);
     hipLaunchKernelGGL(k1_lean, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1439,7 +1439,7 @@ bool lds_store32_in_lane_order() {
 // K1L: long fresh single-Write streams (table <= 4096 entries, positions < 2^31, LDS lane order);
 // EZ_K1L=0 turns it off (A/B: K1x's continuation on the general kernel)
 bool long_applies(const CompressArgs &a) {
-    static const bool off = getenv("EZ_K1L") && atoi(getenv("EZ_K1L")) == 0;
+    static const bool off = knob("EZ_K1L", 1) == 0;
     return !off && !a.ring && !a.write_idx && a.start == 0 && a.header && a.hs <= 4096 && a.hs >= 4 && a.max_len > 0 &&
            a.max_len < (1ull << 31) && lds_store32_in_lane_order();
 }
@@ -1449,7 +1449,7 @@ hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
     // streams per wave: one for batches of a few hundred streams (C4s' 64: K1 361 -> 291 ms), else 4
     // (each wave's instructions serve 4 streams; C2's 4,096 streams: 32.3 ms at 4, 33.5 at 2, 38.2 at
     // 1; 1,024 x 1 MiB compressed at 7.3 GiB/s at 1 against 7.6 at 4); EZ_K1L_SPW=1|2|4 overrides
-    static const uint32_t spw_env = getenv("EZ_K1L_SPW") ? (uint32_t)atoi(getenv("EZ_K1L_SPW")) : 0u;
+    static const uint32_t spw_env = (uint32_t)knob("EZ_K1L_SPW", 0);
     const uint32_t S = spw_env == 1 || spw_env == 2 || spw_env == 4 ? spw_env : (a.count <= 256 ? 1u : 4u);
     const uint64_t rcap = rec_cap(a);
     const size_t lds = (size_t)S * (size_t)a.hs * 4;

@@ -254,8 +254,8 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         return hipGetLastError();
     }
     // EZ_K2=exact (experiments): the exact decoder alone
-    static const bool use_exact = getenv("EZ_K2") && strcmp(getenv("EZ_K2"), "exact") == 0;
-    static const uint64_t long_slot = getenv("EZ_K2_LONG") ? (uint64_t)atoll(getenv("EZ_K2_LONG")) : (64u << 10);
+    static const bool use_exact = knob_str("EZ_K2") && strcmp(knob_str("EZ_K2"), "exact") == 0;
+    static const uint64_t long_slot = (uint64_t)knob("EZ_K2_LONG", 64 << 10);
     if (use_exact) {
         DecompressArgs b = a;
         b.slow = nullptr;
@@ -266,7 +266,7 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     if (g_decompress_variant < 0) {
-        const char *v = getenv("EZ_K2");
+        const char *v = knob_str("EZ_K2");
         g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w' : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : 0));
     }
     if (g_decompress_variant == 't') {
@@ -290,14 +290,14 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
     // outrun K2w's wave per stream (1 GiB batches: 16 Ki x 64 KiB 147 vs 101 GiB/s for K2r,
     // 8 Ki x 128 KiB 74 vs 88; streams past 256 KiB stay on K2w, whose wave takes a long stream
     // ~2x faster than one lane)
-    static const uint64_t ring_min = getenv("EZ_K2_RING_MIN") ? (uint64_t)atoll(getenv("EZ_K2_RING_MIN")) : 12288u;
+    static const uint64_t ring_min = (uint64_t)knob("EZ_K2_RING_MIN", 12288);
     const bool ring_ok = a.count >= ring_min && a.max_out <= (256u << 10);
     if (g_decompress_variant == 'w' || (g_decompress_variant == 0 && a.max_out >= long_slot && !ring_ok)) {
         // long streams (slots of 64 KiB and more, C2/C4): too few to give every lane one;
         // K2w gives each a wave, and its hand-overs go to the exact decoder; the long literals
         // it defers are moved last (the exact decoder writes the same bytes for a stream it takes)
         DecompressArgs b = a;
-        static const bool no_defer = getenv("EZ_K2W_DEFER") && atoi(getenv("EZ_K2W_DEFER")) == 0;  // A/B
+        static const bool no_defer = knob("EZ_K2W_DEFER", 1) == 0;  // A/B
         b.defer = no_defer ? nullptr : a.slow + 2 * a.count + 32;
         b.defer_cap = a.count * (uint64_t)kDefSlots;
         if (b.defer && (e = hipMemsetAsync(b.defer, 0, 16, st)) != hipSuccess) return e;

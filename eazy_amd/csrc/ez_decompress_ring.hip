@@ -268,7 +268,7 @@ __global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A, uint32_t
 }  // namespace
 
 hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t st) {
-    static const uint32_t spw = getenv("EZ_K2R_SPW") ? (uint32_t)atoi(getenv("EZ_K2R_SPW")) : 64u;
+    static const uint32_t spw = (uint32_t)knob("EZ_K2R_SPW", 64);
     static bool attr_done = false;
     const size_t lds = (size_t)(kRingBlock / 64) * spw * kRingStride;
     if (!attr_done) {
@@ -279,7 +279,7 @@ hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t st) {
     const uint64_t grid = (a.count + per_block - 1) / per_block;
     // EZ_K2R_FLUSH (A/B): iterations between ring flushes, a power of two <= kMaxFlushPer
     static const uint32_t fper = [] {
-        const uint32_t v = getenv("EZ_K2R_FLUSH") ? (uint32_t)atoi(getenv("EZ_K2R_FLUSH")) : 8u;
+        const uint32_t v = (uint32_t)knob("EZ_K2R_FLUSH", 8);
         return v >= 1 && v <= kMaxFlushPer && (v & (v - 1)) == 0 ? v : 8u;
     }();
     hipLaunchKernelGGL(k2_ring, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a, spw, fper);

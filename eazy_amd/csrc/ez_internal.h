@@ -7,6 +7,17 @@
 
 namespace ez {
 
+// Timing / A-B switches.  Only experiment builds (make exp: -DEZ_KNOBS) read them from the
+// environment; the product library reads no environment and runs the defaults (kernel choices for
+// tests go through ez_select_compress_kernel / ez_select_decompress_kernel).
+#ifdef EZ_KNOBS
+const char *knob_str(const char *name);
+int knob(const char *name, int dflt);
+#else
+inline const char *knob_str(const char *) { return nullptr; }
+inline int knob(const char *, int dflt) { return dflt; }
+#endif
+
 // K1x per-stream state (ez_compress_spec.hip): speculation restarts at `from`, the pending literal
 // starts at `done`, the stream's output so far is `op` bytes; flags: 0 active, 1 finished
 struct SpecState {

@@ -5,6 +5,8 @@ set -o pipefail
 O=$GRAFT_REPO_ROOT/gpurun_out/abq
 rm -rf $O && mkdir -p $O
 W=$1; shift
+# arms set environment knobs, which only experiment builds read (make -C eazy_amd exp X=0)
+export EZ_LIB=${EZ_LIB:-$GRAFT_REPO_ROOT/eazy_amd/libeazy_amd_x0.so}
 for r in $(seq 1 ${REPS:-1}); do
 k=0
 for ARM in "$@"; do
