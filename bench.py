@@ -146,8 +146,11 @@ def load_traffic(path, workload, count, size, dom):
     else:
         t = json.load(open(path))
     kern = t.get("kernels", t)
-    pre = {"k1_compress": "k1_", "k2_decompress": "k2_", "k3_pack": "k3_"}[dom]
-    vals = [v["traffic"] for k, v in kern.items() if k.startswith(pre) and v.get("traffic")]
+    # the stage's kernels: K1 = the parses and writers (k1_*) and K1x's rounds (kx_*); K2 = the decoders
+    # (k2_*) and the deferred-literal copy (kd_copy); K3 = k3_*; per step (a kernel a step runs several
+    # times counts every dispatch)
+    pre = {"k1_compress": ("k1_", "kx_"), "k2_decompress": ("k2_", "kd_"), "k3_pack": ("k3_",)}[dom]
+    vals = [v.get("per_step", v["traffic"]) for k, v in kern.items() if k.startswith(pre) and v.get("traffic")]
     src = os.path.relpath(path, ROOT) if path.startswith(ROOT) else path
     return (sum(vals) if vals else None), f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, {src}"
 

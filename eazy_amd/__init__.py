@@ -167,8 +167,8 @@ def select_compress_kernel(kind: str = "") -> None:
 
 
 def select_decompress_kernel(kind: str = "") -> None:
-    """Force the first K2 kernel of later batch decodes ('r' ring, 'w' wave;
-    '' = automatic).  Tests and A/B measurement only."""
+    """Force the first K2 kernel of later batch decodes ('r' ring, 't' token-parallel wave per
+    stream, 'w' wave per stream; '' = automatic).  Tests and A/B measurement only."""
     _check(_lib().ez_select_decompress_kernel(ord(kind) if kind else 0))
 
 

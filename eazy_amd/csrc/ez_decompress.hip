@@ -269,7 +269,12 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         const char *v = knob_str("EZ_K2");
         g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w' : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : 0));
     }
-    if (g_decompress_variant == 't') {
+    // Slots of 64 KiB and more (C2, C4, the sweep's long streams) go to K2t; shorter ones to K2r's lane
+    // per stream (1 GiB batches, K2 ms, K2r / K2t: 8 KiB 1.89 / 4.99, 16 KiB 1.96 / 4.89, 32 KiB 3.50 /
+    // 5.06, 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5) - / 7.0, 1 MiB (K2w 29.7) -
+    // / 14.4; C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms)
+    const bool long_slots = a.max_out >= long_slot;
+    if (g_decompress_variant == 't' || (g_decompress_variant == 0 && long_slots)) {
         // K2t: token-parallel, a wave per stream; its hand-overs go to the exact decoder, the long
         // literals it defers are moved last (the exact decoder writes the same bytes for a stream it takes)
         DecompressArgs b = a;
@@ -286,16 +291,9 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         if ((e = hipGetLastError()) != hipSuccess) return e;
         return launch_defer_copy(b, st);
     }
-    // K2w for long slots, unless the batch holds enough streams for K2r's lane per stream to
-    // outrun K2w's wave per stream (1 GiB batches: 16 Ki x 64 KiB 147 vs 101 GiB/s for K2r,
-    // 8 Ki x 128 KiB 74 vs 88; streams past 256 KiB stay on K2w, whose wave takes a long stream
-    // ~2x faster than one lane)
-    static const uint64_t ring_min = (uint64_t)knob("EZ_K2_RING_MIN", 12288);
-    const bool ring_ok = a.count >= ring_min && a.max_out <= (256u << 10);
-    if (g_decompress_variant == 'w' || (g_decompress_variant == 0 && a.max_out >= long_slot && !ring_ok)) {
-        // long streams (slots of 64 KiB and more, C2/C4): too few to give every lane one;
-        // K2w gives each a wave, and its hand-overs go to the exact decoder; the long literals
-        // it defers are moved last (the exact decoder writes the same bytes for a stream it takes)
+    if (g_decompress_variant == 'w') {
+        // K2w (forced: tests, A/B): a wave per stream with a scalar token walk; its hand-overs go to
+        // the exact decoder; the long literals it defers are moved last
         DecompressArgs b = a;
         static const bool no_defer = knob("EZ_K2W_DEFER", 1) == 0;  // A/B
         b.defer = no_defer ? nullptr : a.slow + 2 * a.count + 32;

@@ -213,8 +213,8 @@ int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t
  * back to the automatic choice.  Not thread-safe against concurrent calls. */
 int ez_select_compress_kernel(int kind);
 /* Testing / A-B measurement: the first K2 kernel of later batch decodes with a
- * workspace ('r' lane-per-stream with an LDS ring of recent output, 'w' wave per
- * stream with LDS input and output rings; 0 = automatic: 'w' for slots of 64 KiB
+ * workspace ('r' lane-per-stream with an LDS ring of recent output, 't' token-parallel wave per
+ * stream, 'w' wave per stream with a scalar token walk; 0 = automatic: 't' for slots of 64 KiB
  * and more, else 'r').  Streams either cannot take go on to the exact decoder. */
 int ez_select_decompress_kernel(int kind);
 

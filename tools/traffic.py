@@ -30,10 +30,16 @@ for f in glob.glob(f"{root}/**/*counter_collection.csv", recursive=True):
     for (k, d, c), v in per.items():
         acc[k][c].append(v * 1024.0)
 res = {}
+# bench steps profiled: K3's gather runs exactly once per step (pack); kernels a step runs several times
+# (K1x's per-round kernels, the general kernel's resume modes) get their per-step sum as well
+steps = len(acc["k3_gather"]["FETCH_SIZE"]) if acc.get("k3_gather") and acc["k3_gather"]["FETCH_SIZE"] else None
 for k, v in acc.items():
     fetch = 2.0 * sum(v["FETCH_SIZE"]) / len(v["FETCH_SIZE"]) if v["FETCH_SIZE"] else None
     write = sum(v["WRITE_SIZE"]) / len(v["WRITE_SIZE"]) if v["WRITE_SIZE"] else None
-    res[k] = {"fetch": fetch, "write": write, "traffic": (fetch or 0) + (write or 0) if fetch is not None and write is not None else None}
+    tr = (fetch or 0) + (write or 0) if fetch is not None and write is not None else None
+    disp = len(v["FETCH_SIZE"]) or len(v["WRITE_SIZE"])
+    res[k] = {"fetch": fetch, "write": write, "traffic": tr, "dispatches": disp,
+              "per_step": tr * disp / steps if tr is not None and steps else None}
 if meta:
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     import bench
