@@ -253,6 +253,7 @@ struct ez_writer {
     int last_panic = EZ_PANIC_NONE;  // the reference panic behind the last EZ_EINVAL
     // dev: [input | in_off[2] out_off[2] out_size status write_idx[2] | write_end[k] | write_out[k] | output]
     DBuf ring, ht, dev;
+    DBuf recs;             // K1L's match records (single Writes, ez::long_ring_applies)
     HBuf host;             // the same layout, pinned
     hipStream_t stream = nullptr;
 };
@@ -305,6 +306,7 @@ extern "C" void ez_writer_free(ez_writer *w) {
     w->ring.release();
     w->ht.release();
     w->dev.release();
+    w->recs.release();
     w->host.release();
     if (w->stream) (void)hipStreamDestroy(w->stream);
     delete w;
@@ -338,6 +340,104 @@ namespace {
 // w.b, Write j's bytes ending at out[out_ends[j]].  One host->device copy (the Writes and the
 // launch metadata, from pinned staging), the general kernel with the handle's ring and table,
 // one device->host copy (status, sizes and bytes), one synchronisation.
+// The handle's args for Write j of k (K1L path): stream position, header on a pristine stream's first
+ez::CompressArgs long_args(const ez_writer *w, uint8_t *D, uint64_t *dm, size_t j, uint64_t len, int64_t start) {
+    ez::CompressArgs a{};
+    a.in = D;
+    a.in_off = dm;
+    a.out = D;
+    a.out_off = dm + 2;
+    a.out_size = dm + 4;
+    a.status = (int32_t *)(dm + 5);
+    a.count = 1;
+    a.bs = w->bs;
+    a.hs = w->hs;
+    a.append_magic = w->append_magic;
+    a.ver = w->ver;
+    a.header = w->pristine && j == 0 ? 1 : 0;
+    a.start = start;
+    a.ring = w->ring.as<uint8_t>();
+    a.ht_global = w->ht.as<uint32_t>();
+    a.max_len = len;
+    return a;
+}
+
+// k Writes (k >= 1) through K1L on the handle's ring and table, one after another on the handle's
+// HIP stream (the parse, the token writer and the ring update of each, no host round trip between
+// them): one host->device copy, one device->host copy and one synchronisation for all of them.
+// Returns -1 when a Write does not qualify (ez::long_ring_applies): the caller takes the general kernel.
+int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, uint8_t *out, size_t cap, uint64_t *out_ends,
+                    size_t bound) {
+    if (ez::compress_forced_general()) return -1;
+    DeviceGuard g(w->device);
+    if (!g.ok) return EZ_EDEVICE;
+    const size_t n = (size_t)ends[k - 1];
+    uint64_t recmax = 0;
+    for (size_t j = 0; j < k; j++) {
+        const uint64_t len = ends[j] - (j ? ends[j - 1] : 0);
+        const ez::CompressArgs a = long_args(w, nullptr, nullptr, j, len, w->pos + (int64_t)(j ? ends[j - 1] : 0));
+        if (!ez::long_ring_applies(a)) return -1;
+        const uint64_t r = ez::long_ring_scratch_bytes(a);
+        recmax = r > recmax ? r : recmax;
+    }
+    // [input | per Write: in_off[2] out_off[2] out_size status | outputs, Write j's at its bound prefix]
+    const size_t o_meta = (n + 15) & ~(size_t)15;
+    const size_t o_o = (o_meta + 6 * 8 * k + 15) & ~(size_t)15;
+    const size_t total = o_o + bound + 16;
+    if (w->dev.ensure(total) || w->host.ensure(total) || w->recs.ensure((size_t)recmax)) return EZ_EDEVICE;
+    uint8_t *H = w->host.as<uint8_t>(), *D = w->dev.as<uint8_t>();
+    memcpy(H, p, n);
+    uint64_t *m = (uint64_t *)(H + o_meta);
+    size_t boff = 0;
+    for (size_t j = 0; j < k; j++) {
+        const uint64_t len = ends[j] - (j ? ends[j - 1] : 0);
+        const size_t b = ez_compress_bound((size_t)len);
+        uint64_t *mj = m + 6 * j;
+        mj[0] = j ? ends[j - 1] : 0;
+        mj[1] = ends[j];
+        mj[2] = o_o + boff;
+        mj[3] = o_o + boff + b;
+        mj[4] = 0;
+        mj[5] = 0;
+        boff += b;
+    }
+    EZ_HIP(hipMemcpyAsync(D, H, o_meta + 6 * 8 * k, hipMemcpyHostToDevice, w->stream));
+    hipError_t he = hipSuccess;
+    for (size_t j = 0; j < k && he == hipSuccess; j++) {
+        const uint64_t len = ends[j] - (j ? ends[j - 1] : 0);
+        const ez::CompressArgs a = long_args(w, D, (uint64_t *)(D + o_meta) + 6 * j, j, len, w->pos + (int64_t)(j ? ends[j - 1] : 0));
+        he = ez::launch_long_ring(a, w->recs.as<uint8_t>(), w->stream);
+    }
+    if (he == hipSuccess) he = hipMemcpyAsync(H + o_meta, D + o_meta, o_o - o_meta + bound, hipMemcpyDeviceToHost, w->stream);
+    if (he == hipSuccess) he = hipStreamSynchronize(w->stream);
+    if (he != hipSuccess) {
+        (void)writer_zero(w);
+        return EZ_EDEVICE;
+    }
+    int st = EZ_OK;
+    size_t got = 0;
+    for (size_t j = 0; j < k && !st; j++) {
+        st = (int)(int32_t)(m[6 * j + 5] & 0xffffffffu);
+        got += (size_t)m[6 * j + 4];
+    }
+    if (!st && got > cap) st = EZ_ENOSPC;  // cannot happen (cap >= the sum of the bounds)
+    if (st) {
+        if (st == EZ_EINVAL) w->last_panic = EZ_PANIC_OFFSET;  // (Writes of < 2^26 bytes: no length panic)
+        const int z = writer_zero(w);
+        return z ? z : st;
+    }
+    size_t at = 0;
+    for (size_t j = 0; j < k; j++) {
+        const size_t sz = (size_t)m[6 * j + 4];
+        if (sz) memcpy(out + at, H + (size_t)m[6 * j + 2], sz);
+        at += sz;
+        if (out_ends) out_ends[j] = at;
+    }
+    w->pos += (int64_t)n;
+    w->pristine = false;
+    return EZ_OK;
+}
+
 int writer_run(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, uint8_t *out, size_t cap, uint64_t *out_ends) {
     const size_t n = k ? (size_t)ends[k - 1] : 0;
     size_t bound = 0;
@@ -348,6 +448,10 @@ int writer_run(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, u
     // checked before anything reaches the device: the kernel advances the handle's ring and table, so a
     // call that could not return its bytes must not run at all (a retry then sees the same history)
     if (cap < bound) return EZ_ENOSPC;
+    if (k >= 1) {  // K1L on the handle's ring and table, when every Write qualifies
+        const int e = writer_run_long(w, p, ends, k, out, cap, out_ends, bound);
+        if (e >= 0) return e;
+    }
     DeviceGuard g(w->device);
     if (!g.ok) return EZ_EDEVICE;
     const size_t o_meta = (n + 15) & ~(size_t)15, nm = 8 + 2 * k;  // meta words

@@ -711,17 +711,24 @@ uint64_t compress_scratch_words(const CompressArgs &a) {
 static int g_forced_variant = -1;  // -1: not read yet; 0: automatic; else the kernel's letter
 void select_compress_variant(int v) { g_forced_variant = v; }
 
-char compress_variant(const CompressArgs &a) {
+static int forced_variant() {
     int &forced = g_forced_variant;
     if (forced < 0) {
         const char *e = knob_str("EZ_K1");
         forced = e && std::string(e) == "general" ? 'w' : (e && std::string(e) == "long" ? 'l' : 0);
     }
+    return forced;
+}
+
+char compress_variant(const CompressArgs &a) {
+    const int forced = forced_variant();
     if (forced == 'w') return 'w';
     if (forced == 'l' && long_applies(a)) return 'l';  // K1L alone (tests, A/B)
     if (split_stride_words(a) != 0 && forced != 'x') return 's';
     return spec_applies(a, forced == 'x') ? 'x' : 'w';
 }
+
+bool compress_forced_general() { return forced_variant() == 'w'; }
 
 hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;

@@ -825,7 +825,8 @@ __device__ __forceinline__ void bytes32_chk(const uint8_t *p, int32_t y, V16 &c0
 }
 // 16 bytes from y of the window's ring image at w.pos = done (bytes y >= done: 0, capped away by
 // trim 2; y < done - bs: stream byte y + bs; before the stream: 0)
-__device__ __forceinline__ V16 ring16(const GW &P, int32_t y, int32_t done, int64_t bs) {
+template <class SRC>
+__device__ __forceinline__ V16 ring16(const SRC &P, int32_t y, int32_t done, int64_t bs) {
     uint64_t lo, hi;
     P.around(y + 8, lo, hi);
     V16 v = keep_low16(V16{lo, hi}, done - y);
@@ -839,8 +840,8 @@ __device__ __forceinline__ V16 ring16(const GW &P, int32_t y, int32_t done, int6
     return v;
 }
 // gext with the long window's ring image on the source side (mode 2: ring16; 0 zeros; 1 stream)
-template <int G>
-__device__ __forceinline__ void gext_long(const GW &P, bool runf, bool runb, int g, int lj, int32_t a, int32_t b, int mode,
+template <int G, class SRC>
+__device__ __forceinline__ void gext_long(const SRC &P, bool runf, bool runb, int g, int lj, int32_t a, int32_t b, int mode,
                                           int32_t done, int64_t bs, int32_t fromf, int32_t limf, int32_t limb, int32_t &resf,
                                           int32_t &resb) {
     constexpr int H = G / 2;
@@ -899,9 +900,94 @@ __device__ __forceinline__ void gext_long(const GW &P, bool runf, bool runb, int
     }
 }
 
+// The history a window match compares against, as a linear byte view (positions relative to the
+// parse's p; ring16 turns it into the ring image).  FreshSrc: a fresh Writer, nothing before p (the
+// zero ring).  RingSrc: a Writer handle's Write at stream position start: the bytes before p are the
+// handle's ring as the Write found it (block[(start + y) & mask]; zeros where the stream
+// has not reached yet), p's own from 0 on.
+struct FreshSrc : GW {
+    __device__ __forceinline__ void bytes32(int32_t cand, V16 &c0, V16 &c1) const {
+        bytes32_chk(p, cand, c0, c1, blo, bhi);
+        c0.lo &= cand >= 8 ? ~0ull : (cand <= 0 ? 0ull : ~0ull << (8 * (8 - cand)));  // before the stream: zeros
+    }
+};
+struct RingSrc {
+    const uint8_t *p, *blo, *bhi;  // the Write (blo = p, bhi = p + n)
+    const uint8_t *ring;
+    int64_t start;
+    uint32_t mask;
+    __device__ __forceinline__ V16 ring_at(int32_t y) const {  // 16 ring bytes of positions y .. y+15 (< 0)
+        const uint32_t r = (uint32_t)((start + y) & mask);
+        if (r + 16 <= mask + 1) return ld16v(ring + r);
+        V16 v{0, 0};
+        for (int t = 0; t < 16; t++) {
+            const uint64_t c = ring[(r + t) & mask];
+            if (t < 8) v.lo |= c << (8 * t);
+            else v.hi |= c << (8 * (t - 8));
+        }
+        return v;
+    }
+    __device__ __forceinline__ void around(int32_t y, uint64_t &before, uint64_t &from) const {
+        V16 v;
+        if (y - 8 >= 0) {
+            const uint8_t *a = p + (y - 8);
+            v = a + 16 <= bhi ? ld16v(a) : ld_clamped(a, blo, bhi);  // (past the Write: 0)
+        } else if (y + 8 <= 0) {
+            v = ring_at(y - 8);
+        } else {  // across the Write's start: the ring's bytes, then p's
+            const V16 r = ring_at(y - 8);
+            const uint8_t *a = p;
+            const V16 q = a + 16 <= bhi ? ld16v(a) : ld_clamped(a, blo, bhi);
+            const uint32_t k = (uint32_t)(8 - y);  // ring bytes (1 .. 15)
+            const V16 qs = shl16(q, k), m = keep_low16(V16{~0ull, ~0ull}, (int32_t)k);
+            v = V16{(r.lo & m.lo) | (qs.lo & ~m.lo), (r.hi & m.hi) | (qs.hi & ~m.hi)};
+        }
+        before = v.lo;
+        from = v.hi;
+    }
+    __device__ __forceinline__ void bytes32(int32_t cand, V16 &c0, V16 &c1) const {
+        around(cand, c0.lo, c0.hi);
+        around(cand + 16, c1.lo, c1.hi);
+    }
+};
+
+// LdsSrc: RingSrc with the Write and the ring's last bytes before it staged in LDS (a handle's Write of
+// at most kLdsWrite bytes): lds + kLdsRing + y holds position y for -rl <= y < n + 64 (zeros past
+// the Write); the window's bytes and the candidates' come from there, anything else from RingSrc.
+constexpr int32_t kLdsRing = 16384, kLdsWrite = 49152;
+typedef uint64_t __attribute__((aligned(1))) u64_ua;
+struct LdsSrc {
+    const uint8_t *lds;
+    int32_t rl, n;
+    RingSrc g;
+    static constexpr bool kWindow = true;  // the window's bytes from here too
+    __device__ __forceinline__ void around(int32_t y, uint64_t &before, uint64_t &from) const {
+        if (y - 8 >= -rl && y + 8 <= n + 64) {
+            const uint8_t *q = lds + kLdsRing + (y - 8);
+            before = *(const u64_ua *)q;
+            from = *(const u64_ua *)(q + 8);
+        } else {
+            g.around(y, before, from);
+        }
+    }
+    __device__ __forceinline__ void bytes32(int32_t cand, V16 &c0, V16 &c1) const {
+        around(cand, c0.lo, c0.hi);
+        around(cand + 16, c1.lo, c1.hi);
+    }
+};
+template <class SRC>
+struct WindowFromSrc {
+    static constexpr bool value = false;
+};
+template <>
+struct WindowFromSrc<LdsSrc> {
+    static constexpr bool value = true;
+};
+
 // the parse of one stream by a 16-lane group from (i, done) with the table in htw
-__device__ __forceinline__ void long_loop(const uint8_t *p, int32_t n, int32_t i, int32_t done, int64_t bs, int lj, int g,
-                                          uint32_t *htw, uint32_t hsh, uint4 *rec, uint64_t rcap, const uint8_t *blo,
+template <class SRC>
+__device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_t n, int32_t i, int32_t done, int64_t bs, int lj,
+                                          int g, uint32_t *htw, uint32_t hsh, uint4 *rec, uint64_t rcap, const uint8_t *blo,
                                           const uint8_t *bhi, int32_t &nrec_out, int &err) {
     constexpr int G = 16;
     int32_t nrec = 0;
@@ -911,10 +997,15 @@ __device__ __forceinline__ void long_loop(const uint8_t *p, int32_t n, int32_t i
     WinDwL wd;
     wd.dw = 0;
     wd.r0 = 0;
-    const GW P{p, blo, bhi};
-    wd.load(p, live ? i : 0, lj, blo, bhi);
+    if (!WindowFromSrc<SRC>::value) wd.load(p, live ? i : 0, lj, blo, bhi);
+    constexpr bool kWinSrc = WindowFromSrc<SRC>::value;
     while (__ballot(live) != 0) {
-        wd.bytes(g, lj, w0, w1);
+        if (kWinSrc) {
+            P.around(i + lj, w0.lo, w0.hi);
+            P.around(i + lj + 16, w1.lo, w1.hi);
+        } else {
+            wd.bytes(g, lj, w0, w1);
+        }
         if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
         const int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
         const int32_t x = i + lj;
@@ -929,8 +1020,7 @@ __device__ __forceinline__ void long_loop(const uint8_t *p, int32_t n, int32_t i
         const bool far = !rl && (int64_t)done - cand > bs;  // writer.go:221-224
         V16 c0{0, 0}, c1{0, 0};
         if (valid && !far) {
-            bytes32_chk(p, cand, c0, c1, blo, bhi);
-            c0.lo &= cand >= 8 ? ~0ull : (cand <= 0 ? 0ull : ~0ull << (8 * (8 - cand)));  // before the stream: the fresh ring's zeros
+            P.bytes32(cand, c0, c1);
             if (!rl && (int64_t)cand - 8 < (int64_t)done - bs) c0.lo = ring16(P, cand - 8, done, bs).lo;  // rare
         }
 
@@ -993,7 +1083,7 @@ __device__ __forceinline__ void long_loop(const uint8_t *p, int32_t n, int32_t i
             const int32_t blim = zra ? ca - done : (rla ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
             const int32_t flim = zra ? n - ca : (rla ? n - xa : ((done - ca) < n - xa ? done - ca : n - xa));
             int32_t fx, cx;
-            gext_long<G>(P, need && (ea & 1), need && (ea & 2), g, lj, fa, ca, mode, done, bs, 24, flim, blim, fx, cx);
+            gext_long<G, SRC>(P, need && (ea & 1), need && (ea & 2), g, lj, fa, ca, mode, done, bs, 24, flim, blim, fx, cx);
             if (need) {
                 int32_t f = (ea & 1) ? fx : fwa;
                 const int32_t c = (ea & 2) ? cx : (zra ? fa - bcast(lit, al) : jba);
@@ -1023,7 +1113,7 @@ __device__ __forceinline__ void long_loop(const uint8_t *p, int32_t n, int32_t i
             i += nvalid;
         }
         if (live && (err || i + 4 > n)) live = false;
-        wd.load(p, live ? i : 0, lj, blo, bhi);  // the next window's bytes
+        if (!kWinSrc) wd.load(p, live ? i : 0, lj, blo, bhi);  // the next window's bytes
     }
     nrec_out = nrec;
 }
@@ -1058,8 +1148,65 @@ __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_wor
         for (int32_t k = lj; k < (int32_t)A.hs; k += G) htw[k] = have && spec ? A.spec_tab[s * (uint64_t)A.hs + k] : 0u;
     int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : (have ? 0 : EZ_EINVAL);
     int32_t nrec = 0;
-    long_loop(p, n, i, done, A.bs, lj, g, htw, hsh, recs + (have ? s * rcap : 0), rcap, blo, bhi, nrec, err);
+    long_loop(FreshSrc{{p, blo, bhi}}, p, n, i, done, A.bs, lj, g, htw, hsh, recs + (have ? s * rcap : 0), rcap, blo, bhi, nrec, err);
     if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
+}
+
+// K1L on a Writer handle (Writer.Write writer.go:206-337 on a stream at position start): one 16-lane
+// group, the handle's table (uint32 stream positions) in LDS as positions relative to the Write (far
+// ones clamped: the far skip, writer.go:219-221, still sees them as far), the history before the Write
+// from the handle's ring (RingSrc).  The table goes back to the handle, converted back, at the end.
+constexpr int32_t kRelFar = 1 << 28;  // |relative position| clamp (bs <= 2^26, Writes < 2^27 bytes)
+template <bool LDS>
+__global__ __launch_bounds__(64) void k1_long_ring(CompressArgs A, uint4 *recs, uint64_t rcap) {
+    constexpr int G = 16;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = (int)(threadIdx.x & 63);
+    const int g = lane / G, lj = lane % G;
+    const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(A.hs - 1)));
+    uint32_t *htw = (uint32_t *)smem;
+    const uint8_t *p = A.in + A.in_off[0];
+    const int32_t n = (int32_t)(A.in_off[1] - A.in_off[0]);
+    uint8_t *lds = smem + (size_t)A.hs * 4;
+    const int32_t rl = A.bs < kLdsRing ? (int32_t)A.bs : kLdsRing;
+    const uint32_t mask = (uint32_t)(A.bs - 1);
+    if (LDS) {  // the ring's last rl bytes, the Write, 64 zeros: 16 bytes per lane and step
+        const RingSrc R{p, p, p + n, A.ring, A.start, mask};
+        for (int32_t y = -rl + 16 * lane; y < n + 64; y += 16 * 64) {
+            V16 v;
+            if (y < 0) v = R.ring_at(y);  // (rl is a multiple of 16: no piece straddles the Write's start)
+            else v = p + y + 16 <= p + n ? ld16v(p + y) : (y < n ? ld_clamped(p + y, p, p + n) : V16{0, 0});
+            *(u64_ua *)(lds + kLdsRing + y) = v.lo;
+            *(u64_ua *)(lds + kLdsRing + y + 8) = v.hi;
+        }
+        __syncthreads();
+    }
+    if (g != 0) return;  // one group (the other lanes idle)
+    for (int32_t k = lj; k < (int32_t)A.hs; k += G) {
+        int64_t r = (int64_t)A.ht_global[k] - A.start;
+        r = r < -kRelFar ? -kRelFar : (r > kRelFar ? kRelFar : r);
+        htw[k] = (uint32_t)(int32_t)r;
+    }
+    int err = 0;
+    int32_t nrec = 0;
+    const RingSrc P{p, p, p + n, A.ring, A.start, mask};
+    if (LDS) long_loop(LdsSrc{lds, rl, n, P}, p, n, 0, 0, A.bs, lj, 0, htw, hsh, recs, rcap, p, p + n, nrec, err);
+    else long_loop(P, p, n, 0, 0, A.bs, lj, 0, htw, hsh, recs, rcap, p, p + n, nrec, err);
+    for (int32_t k = lj; k < (int32_t)A.hs; k += G) {
+        const int32_t r = (int32_t)htw[k];
+        if (r != -kRelFar && r != kRelFar) A.ht_global[k] = (uint32_t)(A.start + r);
+    }
+    if (lj == 0) A.out_size[0] = (uint64_t)nrec | ((uint64_t)err << 48);
+}
+
+// the Write's last min(n, bs) bytes into the handle's ring (block[(start + k) & mask], copyData)
+__global__ __launch_bounds__(256) void k1_ring_store(CompressArgs A) {
+    const uint8_t *p = A.in + A.in_off[0];
+    const int64_t n = (int64_t)(A.in_off[1] - A.in_off[0]);
+    const int64_t from = n > A.bs ? n - A.bs : 0;
+    const uint64_t mask = (uint64_t)A.bs - 1;
+    for (int64_t k = from + (int64_t)(blockIdx.x * 256 + threadIdx.x); k < n; k += (int64_t)gridDim.x * 256)
+        A.ring[(uint64_t)(A.start + k) & mask] = p[k];
 }
 
 // Edge slots (after the records in the K1 scratch): a zeroed 128-byte dummy region for lane groups
@@ -1159,7 +1306,7 @@ __global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t
     const uint64_t *rec = recs + s * rcap;
 
     // header (writer.go:495-517): magic + reset, or reset alone
-    const int32_t H = spec ? (int32_t)A.spec[s].op : (A.append_magic ? 9 : 3);
+    const int32_t H = spec ? (int32_t)A.spec[s].op : (A.header ? (A.append_magic ? 9 : 3) : 0);
     if (!spec && H > cap) {
         if (lane == 0) {
             A.out_size[s] = 0;
@@ -1167,7 +1314,7 @@ __global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t
         }
         return;
     }
-    if (lane == 0 && !spec) {
+    if (lane == 0 && !spec && H > 0) {
         const int32_t bsl = (int32_t)__builtin_ctzll((uint64_t)A.bs);
         const uint64_t hm = A.append_magic ? (0x141080797a616502ull << 8 | 0x80) : (0x80ull | 0x10ull << 8 | (uint64_t)bsl << 16);
         const V16 hv{hm, A.append_magic ? (uint64_t)bsl : 0ull};
@@ -1463,6 +1610,38 @@ hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k1_emit<true>, dim3((unsigned)((a.count + 3) / 4)), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
+    return hipGetLastError();
+}
+
+// K1L for one Write on a Writer handle (writer_run): single Writes of 16 bytes .. 64 MiB on
+// handles with version 0, a table of at most 4096 entries, bs <= 2^26, positions below 2^32
+// (the uint32 table values stay exact: a Write across 2^32 takes the general kernel)
+bool long_ring_applies(const CompressArgs &a) {
+    return a.count == 1 && a.ring && !a.write_idx && a.ver == 0 && a.hs <= 4096 && a.hs >= 4 && a.bs <= (1ll << 26) &&
+           a.max_len >= 16 && a.max_len < (1ull << 26) && a.start >= 0 && (uint64_t)a.start + a.max_len <= (1ull << 32) &&
+           lds_store32_in_lane_order();
+}
+uint64_t long_ring_scratch_bytes(const CompressArgs &a) { return rec_cap(a) * sizeof(WideRec); }
+hipError_t launch_long_ring(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
+    const uint64_t rcap = rec_cap(a);
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void *)k1_long_ring<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_done = true;
+    }
+    // Writes of up to kLdsWrite bytes: the Write and the ring's last bytes in LDS
+    if (a.max_len <= (uint64_t)kLdsWrite)
+        hipLaunchKernelGGL(k1_long_ring<true>, dim3(1), dim3(64), (size_t)a.hs * 4 + kLdsRing + kLdsWrite + 64, st, a, (uint4 *)recs,
+                           rcap);
+    else
+        hipLaunchKernelGGL(k1_long_ring<false>, dim3(1), dim3(64), (size_t)a.hs * 4, st, a, (uint4 *)recs, rcap);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k1_emit<true>, dim3(1), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const uint64_t n = a.max_len;
+    const uint64_t blocks = (n < (uint64_t)a.bs ? n : (uint64_t)a.bs) / 256 / 16 + 1;
+    hipLaunchKernelGGL(k1_ring_store, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, st, a);
     return hipGetLastError();
 }
 

@@ -130,6 +130,11 @@ void select_compress_variant(int v);  // 0 = automatic, else a variant letter (t
 bool long_applies(const CompressArgs &a);
 uint64_t long_scratch_bytes(const CompressArgs &a);
 hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t s);
+// K1L on a Writer handle's single Write (the handle's ring as history, its table in and out)
+bool long_ring_applies(const CompressArgs &a);
+uint64_t long_ring_scratch_bytes(const CompressArgs &a);
+hipError_t launch_long_ring(const CompressArgs &a, uint8_t *recs, hipStream_t s);
+bool compress_forced_general();  // ez_select_compress_kernel('w') (tests, A/B)
 // K1x: the data-parallel first pass for long fresh single-Write streams (ez_compress_spec.hip)
 bool spec_applies(const CompressArgs &a, bool any_len = false);  // any_len: also below 64 KiB (forced)
 uint64_t spec_scratch_bytes(const CompressArgs &a);

@@ -424,3 +424,36 @@ def test_write_batch_short_sink_write(cuda):
                 w.Write(p)
         calls.append(s.calls)
     assert calls[1] == calls[0]
+
+
+@pytest.mark.parametrize("block,ht", [(1 << 20, 1024), (4096, 4096), (65536, 256), (1024, 16)])
+def test_handle_writes_k1l_and_general(cuda, block, ht):
+    """Writer.Write on a handle takes K1L on the handle's ring and table (the Write and the ring's
+    last 16 KiB staged in LDS up to 48 KiB Writes, global reads past that); the general kernel
+    forced gives the same stream.  Writes of 20 B .. 200 KiB of logs and random bytes with planted
+    repeats, windows of 1 KiB .. 1 MiB (far skips, the ring wrapping inside a Write, Writes longer
+    than the window); the sink equals the oracle's for the same Writes."""
+    import eazy_amd as ez
+    import oracle as orc
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(block + ht)
+    d = synth.logs(77, 1 << 20).tobytes()
+    r = rng.integers(0, 256, 1 << 18, dtype=np.uint8).tobytes()
+    writes = [d[:20], d[20:5000], r[:60000], d[5000:205000], r[:3000] + d[:3000], d[205000:205100], r[1000:71000],
+              d[:50000], d[300000:301000]]
+    outs = []
+    for kind in ("", "w"):
+        ez.select_compress_kernel(kind)
+        try:
+            s = _Sink()
+            w = ez.Writer(s, block, ht)
+            for p in writes:
+                assert w.Write(p) == len(p)
+            w.Flush()
+            outs.append(b"".join(s.calls))
+        finally:
+            ez.select_compress_kernel("")
+    want = orc.compress(block, ht, writes)
+    assert outs[0] == want, "K1L handle path"
+    assert outs[1] == want, "general kernel"
