@@ -115,17 +115,21 @@ def launch_ranks(nproc: int, argv: list[str]) -> int:
 
 def source_hash() -> str:
     """Hash of everything that decides the kernels' code (HIP sources, headers,
-    build flags): PMC traffic measured at one hash is valid for any commit with
-    the same hash."""
+    build flags), comments and blank lines removed: PMC traffic measured at one
+    hash is valid for any commit with the same hash."""
     import glob
     import hashlib
+    import re
 
     h = hashlib.sha256()
     files = sorted(glob.glob(os.path.join(ROOT, "eazy_amd", "csrc", "*"))) + [
         os.path.join(ROOT, "include", "eazy.h"), os.path.join(ROOT, "eazy_amd", "Makefile")]
     for f in files:
+        text = open(f, "rb").read().decode("utf-8", "replace")
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        lines = (re.sub(r"(^|\s)(//|#\s).*$", "", ln).rstrip() for ln in text.splitlines())
         h.update(os.path.basename(f).encode())
-        h.update(open(f, "rb").read())
+        h.update("\n".join(ln for ln in lines if ln).encode())
     return h.hexdigest()[:16]
 
 

@@ -16,10 +16,12 @@
 //     and every lane computes, for each of its 16 input positions, how many input
 //     bytes a token starting there would take (SWAR over 4 positions a word; the
 //     common forms only, 0 for the others);
-//  2. walk: the scalar unit follows the chain from the window's entry through
-//     those advances (one v_readlane and a few scalar instructions per token;
-//     the rare forms are parsed in full when the walk reaches them), marking the
-//     real token starts in per-row masks;
+//  2. walk: each lane follows the chain through its own 16 positions from every
+//     entry offset (backwards, so each position's exit from the lane's segment
+//     is one lookup: ex[p]); the scalar unit then crosses the window segment to
+//     segment through those exits (64 steps per window, the rare forms parsed in
+//     full when the walk reaches them), and every lane marks the real token starts
+//     of its segment from the entry the walk gave it;
 //  3. tokens: the starts are compacted into a list; each round gives 64 tokens
 //     one lane each: the full parse (k2_scan), a wave prefix sum of the output
 //     lengths (every token's output position at once), every literal written at
