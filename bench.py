@@ -116,7 +116,9 @@ def launch_ranks(nproc: int, argv: list[str]) -> int:
 def source_hash() -> str:
     """Hash of everything that decides the kernels' code (HIP sources, headers,
     build flags), comments and blank lines removed: PMC traffic measured at one
-    hash is valid for any commit with the same hash."""
+    hash is valid for any commit with the same hash.  Diagnostic-only code (the
+    `#if (EZ_EXP ...)` blocks without an `#else`, EZ_PROF_MARK lines) is left out
+    too: the product build compiles none of it."""
     import glob
     import hashlib
     import re
@@ -127,6 +129,8 @@ def source_hash() -> str:
     for f in files:
         text = open(f, "rb").read().decode("utf-8", "replace")
         text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        text = re.sub(r"#if \(EZ_EXP[^\n]*\n(?:(?!#else|#endif|#if).)*?#endif", "", text, flags=re.S)
+        text = re.sub(r"\n\s*EZ_PROF_MARK\(\d+\);", "", text)
         lines = (re.sub(r"(^|\s)(//|#\s).*$", "", ln).rstrip() for ln in text.splitlines())
         h.update(os.path.basename(f).encode())
         h.update("\n".join(ln for ln in lines if ln).encode())

@@ -999,13 +999,20 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
     wd.r0 = 0;
     if (!WindowFromSrc<SRC>::value) wd.load(p, live ? i : 0, lj, blo, bhi);
     constexpr bool kWinSrc = WindowFromSrc<SRC>::value;
+#if (EZ_EXP & 4)
+    uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime(), prof_it = 0, prof_acc = 0, prof_ef = 0, prof_eb = 0;
+#endif
     while (__ballot(live) != 0) {
+#if (EZ_EXP & 4)
+        prof_it++;
+#endif
         if (kWinSrc) {
             P.around(i + lj, w0.lo, w0.hi);
             P.around(i + lj + 16, w1.lo, w1.hi);
         } else {
             wd.bytes(g, lj, w0, w1);
         }
+        EZ_PROF_MARK(0);
         if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
         const int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
         const int32_t x = i + lj;
@@ -1018,11 +1025,13 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
         const int32_t cand = valid ? (d ? x - d : tv) : 0;
         const bool rl = cand >= done && cand < x;
         const bool far = !rl && (int64_t)done - cand > bs;  // writer.go:221-224
+        EZ_PROF_MARK(1);
         V16 c0{0, 0}, c1{0, 0};
         if (valid && !far) {
             P.bytes32(cand, c0, c1);
             if (!rl && (int64_t)cand - 8 < (int64_t)done - bs) c0.lo = ring16(P, cand - 8, done, bs).lo;  // rare
         }
+        EZ_PROF_MARK(2);
 
         // ---- capped judgement, writer.go:219-301 (window) and :441-473 (writeRunlen, cut)
         const uint64_t e0 = w0.hi ^ c0.hi, e1 = w1.lo ^ c1.lo, e2 = w1.hi ^ c1.hi;
@@ -1071,6 +1080,12 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
         const int al = G * g + (a < 0 ? 0 : a);
         int32_t nxt = bcast(nx, al);
         const int32_t ea = bcast(ext, al);
+        EZ_PROF_MARK(3);
+#if (EZ_EXP & 4)
+        prof_acc += act ? 1 : 0;
+        prof_ef += act && (ea & 1) ? 1 : 0;
+        prof_eb += act && (ea & 2) ? 1 : 0;
+#endif
         if (__ballot(act && ea != 0) != 0) {
             // rare: a saturated count; exact lengths by the whole group
             const int32_t xa = i + (a < 0 ? 0 : a);
@@ -1098,6 +1113,7 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
                 }
             }
         }
+        EZ_PROF_MARK(4);
         // ---- table: the visited lanes' positions (the last of a hash wins), then lane a's i+1
         if (valid && (a < 0 || lj <= a)) htw[h] = (uint32_t)x;
         if (act && lj == a) {
@@ -1114,7 +1130,14 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
         }
         if (live && (err || i + 4 > n)) live = false;
         if (!kWinSrc) wd.load(p, live ? i : 0, lj, blo, bhi);  // the next window's bytes
+        EZ_PROF_MARK(5);
     }
+#if (EZ_EXP & 4)
+    if (blockIdx.x < 8 && lj == 0)
+        printf("lprof blk %u g %d it %llu acc %llu ef %llu eb %llu: window %llu visit %llu cload %llu judge %llu ext %llu upd %llu\n", blockIdx.x, g,
+               (unsigned long long)prof_it, (unsigned long long)prof_acc, (unsigned long long)prof_ef, (unsigned long long)prof_eb, (unsigned long long)prof[0], (unsigned long long)prof[1],
+               (unsigned long long)prof[2], (unsigned long long)prof[3], (unsigned long long)prof[4], (unsigned long long)prof[5]);
+#endif
     nrec_out = nrec;
 }
 
