@@ -634,6 +634,20 @@ __device__ __forceinline__ int32_t first_diff24(uint64_t e0, uint64_t e1, uint64
     m = min(m, sat_add(ffbl32((uint32_t)(e2 >> 32)), 160u));
     return (int32_t)min(m >> 3, 24u);
 }
+// the same over 40 bytes: 0 .. 40
+__device__ __forceinline__ int32_t first_diff40(uint64_t e0, uint64_t e1, uint64_t e2, uint64_t e3, uint64_t e4) {
+    uint32_t m = ffbl32((uint32_t)e0);
+    m = min(m, sat_add(ffbl32((uint32_t)(e0 >> 32)), 32u));
+    m = min(m, sat_add(ffbl32((uint32_t)e1), 64u));
+    m = min(m, sat_add(ffbl32((uint32_t)(e1 >> 32)), 96u));
+    m = min(m, sat_add(ffbl32((uint32_t)e2), 128u));
+    m = min(m, sat_add(ffbl32((uint32_t)(e2 >> 32)), 160u));
+    m = min(m, sat_add(ffbl32((uint32_t)e3), 192u));
+    m = min(m, sat_add(ffbl32((uint32_t)(e3 >> 32)), 224u));
+    m = min(m, sat_add(ffbl32((uint32_t)e4), 256u));
+    m = min(m, sat_add(ffbl32((uint32_t)(e4 >> 32)), 288u));
+    return (int32_t)min(m >> 3, 40u);
+}
 // the same over 20 bytes (e2: the last 4): 0 .. 20
 __device__ __forceinline__ int32_t first_diff20(uint64_t e0, uint64_t e1, uint32_t e2) {
     uint32_t m = ffbl32((uint32_t)e0);
@@ -800,28 +814,95 @@ __device__ __forceinline__ uint32_t dw_chk(const uint8_t *w, const uint8_t *lo, 
         if (w + t >= lo && w + t < hi) v |= (uint32_t)w[t] << (8 * t);
     return v;
 }
-struct WinDwL : WinDw {
-    __device__ __forceinline__ void load(const uint8_t *p, int32_t i, int lj, const uint8_t *lo, const uint8_t *hi) {
-        const uintptr_t a = (uintptr_t)(p + i - 8);
-        r0 = (uint32_t)(a & 3);
-        dw = dw_chk((const uint8_t *)((a & ~(uintptr_t)3) + 4 * (uint32_t)lj), lo, hi);
+// K1L's window bytes (x-8 .. x+39 of each lane's x) from a 128-byte region held across windows
+// with the next one in flight (WinRoll's scheme with bounds-checked loads: any stream of any batch)
+struct WinRollL {
+    uint32_t c0, c1, f0, f1;  // this lane's dwords 2k, 2k+1 of the current and the prefetched region
+    int32_t cb, fb, pm;       // region starts relative to p (4-byte aligned addresses); p & 3
+    __device__ __forceinline__ int32_t floor4(int32_t y) const { return y - ((pm + y) & 3); }
+    __device__ __forceinline__ static void ld(const uint8_t *p, int32_t b, int lj, const uint8_t *lo, const uint8_t *hi,
+                                              uint32_t &d0, uint32_t &d1) {
+        const uint8_t *a = p + b + 8 * lj;
+        if (a >= lo && a + 8 <= hi) {
+            typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+            typedef const __attribute__((address_space(1))) u32x2 *gu64p;
+            const u32x2 v = *(gu64p)a;
+            d0 = v.x;
+            d1 = v.y;
+        } else {
+            d0 = dw_chk(a, lo, hi);
+            d1 = dw_chk(a + 4, lo, hi);
+        }
+    }
+    __device__ __forceinline__ void init(const uint8_t *p, int32_t i, int lj, bool live, const uint8_t *lo, const uint8_t *hi) {
+        pm = (int32_t)((uintptr_t)p & 3);
+        cb = floor4(i - 8);
+        fb = cb + 64;
+        c0 = c1 = f0 = f1 = 0;
+        if (live) {
+            ld(p, cb, lj, lo, hi, c0, c1);
+            ld(p, fb, lj, lo, hi, f0, f1);
+        }
+    }
+    // the region for the window at i (group-uniform: 0 <= i - 8 - cb <= 64), after this window's gathers
+    __device__ __forceinline__ void advance(const uint8_t *p, int32_t i, int lj, bool live, const uint8_t *lo, const uint8_t *hi) {
+        const int32_t y = i - 8;
+        if (live && !(y >= cb && y - cb <= 64)) {
+            if (y >= fb && y - fb <= 64) {
+                cb = fb;
+                c0 = f0;
+                c1 = f1;
+            } else {  // a long jump (or back: the cut branch): the region is loaded on the chain
+                cb = floor4(y);
+                ld(p, cb, lj, lo, hi, c0, c1);
+            }
+            fb = cb + 64;
+            ld(p, fb, lj, lo, hi, f0, f1);
+        }
+    }
+    __device__ __forceinline__ void bytes48(int32_t i, int g, int lj, V16 &w0, V16 &w1, V16 &w2) const {
+        const uint32_t o = (uint32_t)(i - 8 - cb + lj), q = o >> 2, r = o & 3;  // o <= 79: q >> 1 <= 9
+        const int src = 4 * (16 * g + (int)(q >> 1));
+        uint32_t e[14];
+#pragma unroll
+        for (int t = 0; t < 7; t++) {
+            e[2 * t] = (uint32_t)__builtin_amdgcn_ds_bpermute(src + 4 * t, (int)c0);
+            e[2 * t + 1] = (uint32_t)__builtin_amdgcn_ds_bpermute(src + 4 * t, (int)c1);
+        }
+        const uint32_t m = 0u - (q & 1);
+        uint32_t d[13];
+#pragma unroll
+        for (int t = 0; t < 13; t++) d[t] = (e[t + 1] & m) | (e[t] & ~m);
+        uint32_t b[12];
+#pragma unroll
+        for (int t = 0; t < 12; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+        w0 = V16{(uint64_t)b[0] | ((uint64_t)b[1] << 32), (uint64_t)b[2] | ((uint64_t)b[3] << 32)};
+        w1 = V16{(uint64_t)b[4] | ((uint64_t)b[5] << 32), (uint64_t)b[6] | ((uint64_t)b[7] << 32)};
+        w2 = V16{(uint64_t)b[8] | ((uint64_t)b[9] << 32), (uint64_t)b[10] | ((uint64_t)b[11] << 32)};
     }
 };
-// bytes y-8 .. y+23 (bytes outside the batch read 0)
-__device__ __forceinline__ void bytes32_chk(const uint8_t *p, int32_t y, V16 &c0, V16 &c1, const uint8_t *lo, const uint8_t *hi) {
+// bytes y-8 .. y+39 (bytes outside the batch read 0)
+__device__ __forceinline__ void bytes48_chk(const uint8_t *p, int32_t y, V16 &c0, V16 &c1, V16 &c2, const uint8_t *lo,
+                                            const uint8_t *hi) {
     const uintptr_t a = (uintptr_t)(p + y - 8);
     const uint8_t *w = (const uint8_t *)(a & ~(uintptr_t)3);
-    if (w >= lo && w + 36 <= hi) {
-        bytes32(LeanIn{}, p, y, c0, c1);
-        return;
-    }
     const uint32_t r = (uint32_t)(a & 3);
-    uint32_t d[9];
-    for (int t = 0; t < 9; t++) d[t] = dw_chk(w + 4 * t, lo, hi);
-    uint32_t b[8];
-    for (int t = 0; t < 8; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+    uint32_t d[13];
+    if (w >= lo && w + 52 <= hi) {
+        const LeanIn L;
+        const uint4 q0 = L.dw4(w), q1 = L.dw4(w + 16), q2 = L.dw4(w + 32);
+        const uint32_t q3 = L.dw(w + 48);
+        d[0] = q0.x, d[1] = q0.y, d[2] = q0.z, d[3] = q0.w, d[4] = q1.x, d[5] = q1.y, d[6] = q1.z, d[7] = q1.w;
+        d[8] = q2.x, d[9] = q2.y, d[10] = q2.z, d[11] = q2.w, d[12] = q3;
+    } else {
+        for (int t = 0; t < 13; t++) d[t] = dw_chk(w + 4 * t, lo, hi);
+    }
+    uint32_t b[12];
+#pragma unroll
+    for (int t = 0; t < 12; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
     c0 = V16{(uint64_t)b[0] | ((uint64_t)b[1] << 32), (uint64_t)b[2] | ((uint64_t)b[3] << 32)};
     c1 = V16{(uint64_t)b[4] | ((uint64_t)b[5] << 32), (uint64_t)b[6] | ((uint64_t)b[7] << 32)};
+    c2 = V16{(uint64_t)b[8] | ((uint64_t)b[9] << 32), (uint64_t)b[10] | ((uint64_t)b[11] << 32)};
 }
 // 16 bytes from y of the window's ring image at w.pos = done (bytes y >= done: 0, capped away by
 // trim 2; y < done - bs: stream byte y + bs; before the stream: 0)
@@ -906,8 +987,8 @@ __device__ __forceinline__ void gext_long(const SRC &P, bool runf, bool runb, in
 // handle's ring as the Write found it (block[(start + y) & mask]; zeros where the stream
 // has not reached yet), p's own from 0 on.
 struct FreshSrc : GW {
-    __device__ __forceinline__ void bytes32(int32_t cand, V16 &c0, V16 &c1) const {
-        bytes32_chk(p, cand, c0, c1, blo, bhi);
+    __device__ __forceinline__ void bytes48(int32_t cand, V16 &c0, V16 &c1, V16 &c2) const {
+        bytes48_chk(p, cand, c0, c1, c2, blo, bhi);
         c0.lo &= cand >= 8 ? ~0ull : (cand <= 0 ? 0ull : ~0ull << (8 * (8 - cand)));  // before the stream: zeros
     }
 };
@@ -945,9 +1026,10 @@ struct RingSrc {
         before = v.lo;
         from = v.hi;
     }
-    __device__ __forceinline__ void bytes32(int32_t cand, V16 &c0, V16 &c1) const {
+    __device__ __forceinline__ void bytes48(int32_t cand, V16 &c0, V16 &c1, V16 &c2) const {
         around(cand, c0.lo, c0.hi);
         around(cand + 16, c1.lo, c1.hi);
+        around(cand + 32, c2.lo, c2.hi);
     }
 };
 
@@ -959,8 +1041,7 @@ typedef uint64_t __attribute__((aligned(1))) u64_ua;
 struct LdsSrc {
     const uint8_t *lds;
     int32_t rl, n;
-    RingSrc g;
-    static constexpr bool kWindow = true;  // the window's bytes from here too
+    RingSrc g;  // (the window's bytes come from here too: WindowFromSrc)
     __device__ __forceinline__ void around(int32_t y, uint64_t &before, uint64_t &from) const {
         if (y - 8 >= -rl && y + 8 <= n + 64) {
             const uint8_t *q = lds + kLdsRing + (y - 8);
@@ -970,9 +1051,10 @@ struct LdsSrc {
             g.around(y, before, from);
         }
     }
-    __device__ __forceinline__ void bytes32(int32_t cand, V16 &c0, V16 &c1) const {
+    __device__ __forceinline__ void bytes48(int32_t cand, V16 &c0, V16 &c1, V16 &c2) const {
         around(cand, c0.lo, c0.hi);
         around(cand + 16, c1.lo, c1.hi);
+        around(cand + 32, c2.lo, c2.hi);
     }
 };
 template <class SRC>
@@ -984,7 +1066,11 @@ struct WindowFromSrc<LdsSrc> {
     static constexpr bool value = true;
 };
 
-// the parse of one stream by a 16-lane group from (i, done) with the table in htw
+// the parse of one stream by a 16-lane group from (i, done) with the table in htw.  The capped
+// judgement compares 40 bytes forward (k1_lean: 24): the long parse is a latency chain (few streams
+// per SIMD), and at C2 one accepted copy in nine is 24 - 39 bytes long, whose exact extension
+// (gext_long) is a group-wide round trip that every stream of the wave waits for.
+constexpr int32_t kLCap = 40;
 template <class SRC>
 __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_t n, int32_t i, int32_t done, int64_t bs, int lj,
                                           int g, uint32_t *htw, uint32_t hsh, uint4 *rec, uint64_t rcap, const uint8_t *blo,
@@ -993,11 +1079,9 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
     int32_t nrec = 0;
     bool live = !err && i + 4 <= n;
     int64_t guard = 4 * (int64_t)n + 64;
-    V16 w0{0, 0}, w1{0, 0};  // bytes x-8 .. x+7 and x+8 .. x+23 of this lane's position x
-    WinDwL wd;
-    wd.dw = 0;
-    wd.r0 = 0;
-    if (!WindowFromSrc<SRC>::value) wd.load(p, live ? i : 0, lj, blo, bhi);
+    V16 w0{0, 0}, w1{0, 0}, w2{0, 0};  // bytes x-8 .. x+7, x+8 .. x+23, x+24 .. x+39 of this lane's position x
+    WinRollL wr;
+    if (!WindowFromSrc<SRC>::value) wr.init(p, i, lj, live, blo, bhi);
     constexpr bool kWinSrc = WindowFromSrc<SRC>::value;
 #if (EZ_EXP & 4)
     uint64_t prof[8] = {0, 0, 0, 0, 0, 0, 0, 0}, prof_t = __builtin_amdgcn_s_memtime(), prof_it = 0, prof_acc = 0, prof_ef = 0, prof_eb = 0;
@@ -1009,8 +1093,9 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
         if (kWinSrc) {
             P.around(i + lj, w0.lo, w0.hi);
             P.around(i + lj + 16, w1.lo, w1.hi);
+            P.around(i + lj + 32, w2.lo, w2.hi);
         } else {
-            wd.bytes(g, lj, w0, w1);
+            wr.bytes48(i, g, lj, w0, w1, w2);
         }
         EZ_PROF_MARK(0);
         if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
@@ -1026,16 +1111,15 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
         const bool rl = cand >= done && cand < x;
         const bool far = !rl && (int64_t)done - cand > bs;  // writer.go:221-224
         EZ_PROF_MARK(1);
-        V16 c0{0, 0}, c1{0, 0};
+        V16 c0{0, 0}, c1{0, 0}, c2{0, 0};
         if (valid && !far) {
-            P.bytes32(cand, c0, c1);
+            P.bytes48(cand, c0, c1, c2);
             if (!rl && (int64_t)cand - 8 < (int64_t)done - bs) c0.lo = ring16(P, cand - 8, done, bs).lo;  // rare
         }
         EZ_PROF_MARK(2);
 
         // ---- capped judgement, writer.go:219-301 (window) and :441-473 (writeRunlen, cut)
-        const uint64_t e0 = w0.hi ^ c0.hi, e1 = w1.lo ^ c1.lo, e2 = w1.hi ^ c1.hi;
-        int32_t jf = first_diff24(e0, e1, e2);
+        int32_t jf = first_diff40(w0.hi ^ c0.hi, w1.lo ^ c1.lo, w1.hi ^ c1.hi, w2.lo ^ c2.lo, w2.hi ^ c2.hi);
         jf = jf < n - x ? jf : n - x;
         int32_t bl = x - done;
         if (rl) bl = bl < cand ? bl : cand;
@@ -1052,14 +1136,14 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
         int32_t lit, nx, dist, ext;
         bool force = false;
         if (zr) {  // writeZeros :407-439
-            int32_t zf = first_diff24(0, c1.lo, c1.hi);
+            int32_t zf = first_diff40(0, c1.lo, c1.hi, c2.lo, c2.hi);
             zf = zf < n - cand ? zf : n - cand;
             int32_t zb = last_diff8(c0.lo);
             zb = zb < cand - done ? zb : cand - done;
             lit = cand - zb;
             nx = cand + zf;
             dist = 0;
-            ext = (zf == 24 && n - cand > 24 ? 1 : 0) | (zb == 8 && cand - done > 8 ? 2 : 0);
+            ext = (zf == kLCap && n - cand > kLCap ? 1 : 0) | (zb == 8 && cand - done > 8 ? 2 : 0);
         } else if (cut) {  // the cut branch: a literal to done + i - st, no copy (writer.go:464-473)
             lit = done + (x - cand);
             nx = lit;
@@ -1071,7 +1155,7 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
             dist = x - cand;
             force = rl;
             const int32_t room = rl ? n - x : (done - cand < n - x ? done - cand : n - x);
-            ext = (jf == 24 && room > 24 && (rl || (int64_t)(jb + 24) < t1) ? 1 : 0) | (jb == 8 && bl > 8 ? 2 : 0);
+            ext = (jf == kLCap && room > kLCap && (rl || (int64_t)(jb + kLCap) < t1) ? 1 : 0) | (jb == 8 && bl > 8 ? 2 : 0);
         }
         const uint64_t am64 = __ballot(acc);
         const uint32_t am = (uint32_t)(am64 >> (G * g)) & 0xffffu;
@@ -1098,7 +1182,7 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
             const int32_t blim = zra ? ca - done : (rla ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
             const int32_t flim = zra ? n - ca : (rla ? n - xa : ((done - ca) < n - xa ? done - ca : n - xa));
             int32_t fx, cx;
-            gext_long<G, SRC>(P, need && (ea & 1), need && (ea & 2), g, lj, fa, ca, mode, done, bs, 24, flim, blim, fx, cx);
+            gext_long<G, SRC>(P, need && (ea & 1), need && (ea & 2), g, lj, fa, ca, mode, done, bs, kLCap, flim, blim, fx, cx);
             if (need) {
                 int32_t f = (ea & 1) ? fx : fwa;
                 const int32_t c = (ea & 2) ? cx : (zra ? fa - bcast(lit, al) : jba);
@@ -1129,7 +1213,7 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
             i += nvalid;
         }
         if (live && (err || i + 4 > n)) live = false;
-        if (!kWinSrc) wd.load(p, live ? i : 0, lj, blo, bhi);  // the next window's bytes
+        if (!kWinSrc) wr.advance(p, i, lj, live, blo, bhi);  // the next window's region
         EZ_PROF_MARK(5);
     }
 #if (EZ_EXP & 4)

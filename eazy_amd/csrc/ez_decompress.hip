@@ -236,9 +236,10 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
 
 }  // namespace
 
-// the batch decoders: K2r (ring, slots < 64 KiB) or K2w (wave per stream, longer slots), each
-// handing the streams it does not finish to the exact decoder; 'r' / 'w' force one (tests, A/B)
-static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'r', 'w'
+// the batch decoders: K2r (lane per stream, slots < 64 KiB) or K2t (token-parallel wave per
+// stream, longer slots), each handing the streams it does not finish to the exact decoder; 'r',
+// 't' / 'w' force one (tests, A/B; K2w is reached only this way)
+static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'r', 't', 'w'
 void select_decompress_variant(int v) { g_decompress_variant = v; }
 
 // [slow list: 2 * count + 32 words][K2w's deferred literals: 4 words + count * kDefSlots records]
