@@ -1036,7 +1036,7 @@ struct RingSrc {
 // LdsSrc: RingSrc with the Write and the ring's last bytes before it staged in LDS (a handle's Write of
 // at most kLdsWrite bytes): lds + kLdsRing + y holds position y for -rl <= y < n + 64 (zeros past
 // the Write); the window's bytes and the candidates' come from there, anything else from RingSrc.
-constexpr int32_t kLdsRing = 16384, kLdsWrite = 49152;
+constexpr int32_t kLdsRing = 32768, kLdsWrite = 49152;
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 struct LdsSrc {
     const uint8_t *lds;
@@ -1051,10 +1051,25 @@ struct LdsSrc {
             g.around(y, before, from);
         }
     }
+    __device__ __forceinline__ static V16 lds16(const uint8_t *q) { return V16{*(const u64_ua *)q, *(const u64_ua *)(q + 8)}; }
     __device__ __forceinline__ void bytes48(int32_t cand, V16 &c0, V16 &c1, V16 &c2) const {
-        around(cand, c0.lo, c0.hi);
-        around(cand + 16, c1.lo, c1.hi);
-        around(cand + 32, c2.lo, c2.hi);
+        if (cand - 8 >= -rl && cand + 40 <= n + 64) {  // one check for the 48 bytes
+            const uint8_t *q = lds + kLdsRing + (cand - 8);
+            c0 = lds16(q);
+            c1 = lds16(q + 16);
+            c2 = lds16(q + 32);
+        } else {
+            g.around(cand, c0.lo, c0.hi);
+            g.around(cand + 16, c1.lo, c1.hi);
+            g.around(cand + 32, c2.lo, c2.hi);
+        }
+    }
+    // the window's bytes x-8 .. x+39 (0 <= x < n: always staged)
+    __device__ __forceinline__ void window48(int32_t x, V16 &w0, V16 &w1, V16 &w2) const {
+        const uint8_t *q = lds + kLdsRing + (x - 8);
+        w0 = lds16(q);
+        w1 = lds16(q + 16);
+        w2 = lds16(q + 32);
     }
 };
 template <class SRC>
@@ -1090,10 +1105,8 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
 #if (EZ_EXP & 4)
         prof_it++;
 #endif
-        if (kWinSrc) {
-            P.around(i + lj, w0.lo, w0.hi);
-            P.around(i + lj + 16, w1.lo, w1.hi);
-            P.around(i + lj + 32, w2.lo, w2.hi);
+        if constexpr (kWinSrc) {
+            P.window48(live ? i + lj : 0, w0, w1, w2);
         } else {
             wr.bytes48(i, g, lj, w0, w1, w2);
         }
@@ -1265,11 +1278,11 @@ __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_wor
 // from the handle's ring (RingSrc).  The table goes back to the handle, converted back, at the end.
 constexpr int32_t kRelFar = 1 << 28;  // |relative position| clamp (bs <= 2^26, Writes < 2^27 bytes)
 template <bool LDS>
-__global__ __launch_bounds__(64) void k1_long_ring(CompressArgs A, uint4 *recs, uint64_t rcap) {
+__global__ __launch_bounds__(256) void k1_long_ring(CompressArgs A, uint4 *recs, uint64_t rcap) {
     constexpr int G = 16;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = (int)(threadIdx.x & 63);
-    const int g = lane / G, lj = lane % G;
+    const int tid = (int)threadIdx.x, lane = tid & 63;  // 4 waves stage; wave 0's first group parses
+    const int g = lane / G + 4 * (tid >> 6), lj = lane % G;
     const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(A.hs - 1)));
     uint32_t *htw = (uint32_t *)smem;
     const uint8_t *p = A.in + A.in_off[0];
@@ -1277,33 +1290,60 @@ __global__ __launch_bounds__(64) void k1_long_ring(CompressArgs A, uint4 *recs, 
     uint8_t *lds = smem + (size_t)A.hs * 4;
     const int32_t rl = A.bs < kLdsRing ? (int32_t)A.bs : kLdsRing;
     const uint32_t mask = (uint32_t)(A.bs - 1);
-    if (LDS) {  // the ring's last rl bytes, the Write, 64 zeros: 16 bytes per lane and step
+    if (LDS) {  // the ring's last rl bytes, the Write, 64 zeros: 16 bytes per lane and step, 4 loads in flight
         const RingSrc R{p, p, p + n, A.ring, A.start, mask};
-        for (int32_t y = -rl + 16 * lane; y < n + 64; y += 16 * 64) {
-            V16 v;
-            if (y < 0) v = R.ring_at(y);  // (rl is a multiple of 16: no piece straddles the Write's start)
-            else v = p + y + 16 <= p + n ? ld16v(p + y) : (y < n ? ld_clamped(p + y, p, p + n) : V16{0, 0});
-            *(u64_ua *)(lds + kLdsRing + y) = v.lo;
-            *(u64_ua *)(lds + kLdsRing + y + 8) = v.hi;
+        for (int32_t y0 = -rl + 16 * tid; y0 < n + 64; y0 += 4 * 16 * 256) {
+            V16 v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int32_t y = y0 + u * 16 * 256;
+                if (y < 0) v[u] = R.ring_at(y);  // (rl is a multiple of 16: no piece straddles the Write's start)
+                else v[u] = p + y + 16 <= p + n ? ld16v(p + y) : (y < n ? ld_clamped(p + y, p, p + n) : V16{0, 0});
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int32_t y = y0 + u * 16 * 256;
+                if (y < n + 64) {
+                    *(u64_ua *)(lds + kLdsRing + y) = v[u].lo;
+                    *(u64_ua *)(lds + kLdsRing + y + 8) = v[u].hi;
+                }
+            }
         }
-        __syncthreads();
     }
-    if (g != 0) return;  // one group (the other lanes idle)
-    for (int32_t k = lj; k < (int32_t)A.hs; k += G) {
+    // the table by the whole block (the parse below is one group's)
+#pragma unroll 4
+    for (int32_t k = tid; k < (int32_t)A.hs; k += 256) {
         int64_t r = (int64_t)A.ht_global[k] - A.start;
         r = r < -kRelFar ? -kRelFar : (r > kRelFar ? kRelFar : r);
         htw[k] = (uint32_t)(int32_t)r;
     }
+    __syncthreads();
     int err = 0;
     int32_t nrec = 0;
-    const RingSrc P{p, p, p + n, A.ring, A.start, mask};
-    if (LDS) long_loop(LdsSrc{lds, rl, n, P}, p, n, 0, 0, A.bs, lj, 0, htw, hsh, recs, rcap, p, p + n, nrec, err);
-    else long_loop(P, p, n, 0, 0, A.bs, lj, 0, htw, hsh, recs, rcap, p, p + n, nrec, err);
-    for (int32_t k = lj; k < (int32_t)A.hs; k += G) {
+    if (g == 0) {  // one group (the other lanes idle)
+        const RingSrc P{p, p, p + n, A.ring, A.start, mask};
+        if (LDS) long_loop(LdsSrc{lds, rl, n, P}, p, n, 0, 0, A.bs, lj, 0, htw, hsh, recs, rcap, p, p + n, nrec, err);
+        else long_loop(P, p, n, 0, 0, A.bs, lj, 0, htw, hsh, recs, rcap, p, p + n, nrec, err);
+    }
+    __syncthreads();
+    for (int32_t k = tid; k < (int32_t)A.hs; k += 256) {
         const int32_t r = (int32_t)htw[k];
         if (r != -kRelFar && r != kRelFar) A.ht_global[k] = (uint32_t)(A.start + r);
     }
-    if (lj == 0) A.out_size[0] = (uint64_t)nrec | ((uint64_t)err << 48);
+    if (LDS) {  // the Write into the handle's ring (k1_ring_store's work; the parse has read the ring)
+        const int32_t from = (int64_t)n > A.bs ? (int32_t)(n - A.bs) : 0;
+        for (int32_t k = from + 16 * tid; k < n; k += 16 * 256) {
+            const uint32_t r = (uint32_t)((A.start + k) & mask);
+            const uint8_t *q = lds + kLdsRing + k;
+            if (k + 16 <= n && r + 16 <= mask + 1) {
+                *(u64_ua *)(A.ring + r) = *(const u64_ua *)q;
+                *(u64_ua *)(A.ring + r + 8) = *(const u64_ua *)(q + 8);
+            } else {
+                for (int32_t t = 0; t < 16 && k + t < n; t++) A.ring[(r + (uint32_t)t) & mask] = q[t];
+            }
+        }
+    }
+    if (tid == 0) A.out_size[0] = (uint64_t)nrec | ((uint64_t)err << 48);
 }
 
 // the Write's last min(n, bs) bytes into the handle's ring (block[(start + k) & mask], copyData)
@@ -1738,14 +1778,15 @@ hipError_t launch_long_ring(const CompressArgs &a, uint8_t *recs, hipStream_t st
     }
     // Writes of up to kLdsWrite bytes: the Write and the ring's last bytes in LDS
     if (a.max_len <= (uint64_t)kLdsWrite)
-        hipLaunchKernelGGL(k1_long_ring<true>, dim3(1), dim3(64), (size_t)a.hs * 4 + kLdsRing + kLdsWrite + 64, st, a, (uint4 *)recs,
+        hipLaunchKernelGGL(k1_long_ring<true>, dim3(1), dim3(256), (size_t)a.hs * 4 + kLdsRing + kLdsWrite + 64, st, a, (uint4 *)recs,
                            rcap);
     else
-        hipLaunchKernelGGL(k1_long_ring<false>, dim3(1), dim3(64), (size_t)a.hs * 4, st, a, (uint4 *)recs, rcap);
+        hipLaunchKernelGGL(k1_long_ring<false>, dim3(1), dim3(256), (size_t)a.hs * 4, st, a, (uint4 *)recs, rcap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k1_emit<true>, dim3(1), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
     if ((e = hipGetLastError()) != hipSuccess) return e;
+    if (a.max_len <= (uint64_t)kLdsWrite) return hipSuccess;  // (k1_long_ring<true> stored the ring)
     const uint64_t n = a.max_len;
     const uint64_t blocks = (n < (uint64_t)a.bs ? n : (uint64_t)a.bs) / 256 / 16 + 1;
     hipLaunchKernelGGL(k1_ring_store, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, st, a);
