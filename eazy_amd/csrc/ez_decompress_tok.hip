@@ -486,7 +486,8 @@ __global__ __launch_bounds__(64) void k2_tok(DecompressArgs A) {
 
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t st) {
     const uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);
-    if (a.max_out != 0 && a.max_out <= 4096) {  // the whole stream fits the ring
+    static const int force_r = knob("EZ_K2T_R", 0);  // A/B (experiment builds): 4096 / 8192
+    if (force_r == 4096 || (force_r == 0 && a.max_out != 0 && a.max_out <= 4096)) {  // the whole stream fits the ring
         hipLaunchKernelGGL(k2_tok<4096>, dim3((unsigned)grid), dim3(64), TLayout<4096>::bytes, st, a);
     } else {
         hipLaunchKernelGGL(k2_tok<8192>, dim3((unsigned)grid), dim3(64), TLayout<8192>::bytes, st, a);
