@@ -484,10 +484,26 @@ __global__ __launch_bounds__(64) void k2_tok(DecompressArgs A) {
 
 }  // namespace
 
+// R: an 8 KiB ring keeps more copies in LDS, a 4 KiB one fits more waves per CU (TLayout<4096>
+// ~8.6 KiB, <8192> ~12.7 KiB of LDS).  A batch with more streams than the chip holds runs in
+// rounds of resident waves, the last one partly empty, so R = 4096 is taken whenever it needs
+// fewer such rounds (C2, 4,096 x 256 KiB: 3,072 resident waves at 8 KiB, all 4,096 at 4 KiB:
+// K2 7.06 -> 4.93 ms), and always when the whole stream fits it.
+static uint64_t resident_waves(const void *kernel, size_t lds) {
+    int dev = 0, ncu = 0, per = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, 64, lds) != hipSuccess || per <= 0 || ncu <= 0)
+        return 1;
+    return (uint64_t)per * (uint64_t)ncu;
+}
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t st) {
     const uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);
     static const int force_r = knob("EZ_K2T_R", 0);  // A/B (experiment builds): 4096 / 8192
-    if (force_r == 4096 || (force_r == 0 && a.max_out != 0 && a.max_out <= 4096)) {  // the whole stream fits the ring
+    static const uint64_t res4 = resident_waves((const void *)k2_tok<4096>, TLayout<4096>::bytes);
+    static const uint64_t res8 = resident_waves((const void *)k2_tok<8192>, TLayout<8192>::bytes);
+    const bool fits = a.max_out != 0 && a.max_out <= 4096;  // the whole stream fits the ring
+    const bool fewer_rounds = (grid + res4 - 1) / res4 < (grid + res8 - 1) / res8;
+    if (force_r == 4096 || (force_r == 0 && (fits || fewer_rounds))) {
         hipLaunchKernelGGL(k2_tok<4096>, dim3((unsigned)grid), dim3(64), TLayout<4096>::bytes, st, a);
     } else {
         hipLaunchKernelGGL(k2_tok<8192>, dim3((unsigned)grid), dim3(64), TLayout<8192>::bytes, st, a);

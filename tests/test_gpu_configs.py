@@ -235,3 +235,45 @@ def test_k1x_refused_stream_leaves_others_exact(cuda):
         for s in range(1, 5):
             got = slots[so[s] : so[s] + sz[s]].tobytes()
             assert got == orc.compress(MiB, 1024, [bufs[s]]), f"K1 {kind!r} stream {s}: bytes differ"
+
+
+@pytest.mark.gpu
+def test_k2t_four_kib_ring_on_long_streams(cuda):
+    """K2t takes its 4 KiB ring when that keeps every stream's wave resident at once and the
+    8 KiB one would not (3,072 resident waves with 8 KiB rings on 256 CUs): 3,300 streams of
+    5 - 24 KiB, so copies reach past the ring into output already in HBM and random streams of
+    16 KiB and more defer their one long literal — 't' forced, every stream compared with its
+    input."""
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(71)
+    count = 3300
+    lens = rng.integers(5000, 24577, count)
+    logs = synth.logs(73, int(lens.sum())).tobytes()
+    bufs, at = [], 0
+    for k, n in enumerate(lens):
+        if k % 97 == 0:
+            bufs.append(rng.integers(0, 256, int(n), dtype=np.uint8).tobytes())
+        else:
+            bufs.append(logs[at : at + n])
+            at += n
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    cap = lens + (lens >> 2) + 64
+    slot_off = np.concatenate([[0], np.cumsum(cap)]).astype(np.int64)
+    slots, sizes = orc.compress_batch(MiB, 1024, np.frombuffer(b"".join(bufs), np.uint8).copy(), offs, slot_off, 8)
+    comp = b"".join(slots[slot_off[s] : slot_off[s] + sizes[s]].tobytes() for s in range(count))
+    coff = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    d_comp = torch.from_numpy(np.frombuffer(comp + bytes(64), np.uint8).copy()).to(cuda)
+    ez.select_decompress_kernel("t")
+    try:
+        out, sz, st = ez.decompress_batch(d_comp, torch.from_numpy(coff).to(cuda), torch.from_numpy(offs).to(cuda),
+                                          max_len=int(lens.max()))
+    finally:
+        ez.select_decompress_kernel("")
+    assert st.cpu().abs().sum().item() == 0 and sz.cpu().numpy().tolist() == lens.tolist()
+    got = out[: int(offs[-1])].cpu().numpy().tobytes()
+    for s in range(count):
+        assert got[offs[s] : offs[s + 1]] == bufs[s], f"stream {s} (len {lens[s]}) differs"
