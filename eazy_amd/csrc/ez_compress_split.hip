@@ -73,7 +73,7 @@ using namespace k1;
 __host__ __device__ __forceinline__ uint64_t rec_pack(int32_t lit_end, int32_t clen, int32_t dist, bool force) {
     return (uint64_t)(uint32_t)lit_end | ((uint64_t)(uint32_t)clen << 20) | ((uint64_t)(uint32_t)dist << 40) | ((uint64_t)force << 60);
 }
-constexpr int64_t kMaxT16 = 65535;   // T16 positions fit 16 bits
+constexpr int64_t kMaxT16 = 65536;   // T16 positions fit 16 bits (a stream's visited positions are < n - 3)
 constexpr int64_t kMaxT32 = 1 << 19; // the judgement packs the candidate into 20 bits (and 2n <= block)
 
 // record slot of stream s: s * rec_cap .. ; every match advances done by >= 6,

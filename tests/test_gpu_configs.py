@@ -277,3 +277,18 @@ def test_k2t_four_kib_ring_on_long_streams(cuda):
     got = out[: int(offs[-1])].cpu().numpy().tobytes()
     for s in range(count):
         assert got[offs[s] : offs[s + 1]] == bufs[s], f"stream {s} (len {lens[s]}) differs"
+
+
+@pytest.mark.gpu
+def test_exactly_64k_streams_on_u16_tables(cuda):
+    """Streams of exactly 64 KiB take K1s with u16 tables (visited positions < n - 3 fit 16 bits):
+    logs, random bytes, a sparse stream and a run, byte-compared with the oracle and decoded."""
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(79)
+    d = synth.logs(83, 60 * 65536).tobytes()
+    bufs = [d[k << 16 : (k + 1) << 16] for k in range(60)]
+    sparse = np.frombuffer(rng.integers(0, 256, 65536, dtype=np.uint8).tobytes(), np.uint8).copy()
+    sparse[rng.random(65536) < 0.9] = 0
+    bufs += [rng.integers(0, 256, 65536, dtype=np.uint8).tobytes(), sparse.tobytes(), bytes(65536), (b"abc" * 21846)[:65536]]
+    _gpu_check(cuda, bufs, kinds=("", "S", "l", "w"))
