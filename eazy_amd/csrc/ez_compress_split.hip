@@ -184,8 +184,8 @@ struct Pred<0, ROW> {
 };
 
 // The same search on hashes offset to be nonzero, with DPP bound_ctrl (a lane K below outside the
-// row reads 0, which never equals): the shifted read can fold into the compare (no v_mov of the
-// row-edge default per step)
+// row reads 0, which never equals): no v_mov of the row-edge default per step.  Each step is still
+// v_mov_dpp + v_cmp + v_cndmask: gfx950 has no DPP form of the VOPC compares.
 template <int K>
 struct PredZ {
     __device__ __forceinline__ static int32_t get(uint32_t hp, int32_t d) {
@@ -696,8 +696,8 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         if (cand != 0) {
             if (kFwdCap == 20) bytes28(L, p, cand, c0, c1);
             else bytes32(L, p, cand, c0, c1);
-            // bytes before the stream start are the fresh ring's zeros
-            c0.lo &= cand >= 8 ? ~0ull : ~0ull << (8 * (8 - cand));
+            // bytes before the stream start are the fresh ring's zeros (rare: a branch)
+            if (__builtin_expect(cand < 8, 0)) c0.lo &= ~0ull << (8 * (8 - cand));
         }
         if (prio & 1) __builtin_amdgcn_s_setprio(0);
 
@@ -741,13 +741,8 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         // the group's next position (and whether the acceptor needs an exact extension), one
         // v_readlane per group
         const int32_t pack = nx | (ext << 28);
-        int32_t sel = 0;
-#pragma unroll
-        for (int gg = 0; gg < 64 / G; gg++) {
-            const uint32_t m = (uint32_t)(am64 >> (G * gg)) & 0xffffu;
-            const int32_t v = __builtin_amdgcn_readlane(pack, G * gg + (m ? __builtin_ctz(m) : 0));
-            sel = g == gg ? v : sel;
-        }
+        // (one ds_bpermute from each group's first acceptor: fewer VALU than four v_readlane + selects)
+        const int32_t sel = __builtin_amdgcn_ds_bpermute(4 * (G * g + (a < 0 ? 0 : a)), pack);
         int32_t nxt = sel & 0x0fffffff;
         if (__ballot(act && (sel >> 28) != 0) != 0) {
             // rare: a saturated count; exact lengths by the whole group (as k1_parse)
