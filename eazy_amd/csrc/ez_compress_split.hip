@@ -663,6 +663,24 @@ __device__ __forceinline__ int32_t last_diff8(uint64_t e) {
     return (int32_t)min(m >> 3, 8u);
 }
 
+// Visit by one LDS atomic (MSK): ds_mskor_rtn_b32 sets the lane's u16 table entry to its position
+// and returns the word as it was -- lanes of one wave instruction that hit the same word apply in
+// ascending lane order (probed once per process, k_lds_mskor_order), so a lane reads the position
+// of the nearest earlier lane of its window with the same hash, or the table's entry when there is
+// none: the table read, the 15-step DPP predecessor search and the visited lanes' table store in
+// one instruction.  Lanes after the window's acceptor, which Go never visits, then put back what
+// they found unless it is a position of another such lane (only the first of a hash past the
+// acceptor restores; its value is the one Go's table holds).  (The wait is in the asm: the
+// compiler does not count an asm's LDS operation.)
+__device__ __forceinline__ uint32_t lds_mskor16(uint16_t *hth, uint32_t h, uint32_t val) {
+    const uint32_t sh = (h & 1u) << 4;
+    const uint32_t addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t *)hth) + ((h >> 1) << 2);
+    uint32_t r;
+    asm volatile("ds_mskor_rtn_b32 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr), "v"(0xffffu << sh), "v"(val << sh) : "memory");
+    return (r >> sh) & 0xffffu;
+}
+
+template <bool MSK>
 __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int32_t n, int lj, int g, uint16_t *hth,
                                           uint32_t hsh, uint64_t *rec, uint64_t rcap, int prio, int32_t &nrec_out, int &err) {
     constexpr int G = 16;
@@ -689,9 +707,14 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         // ---- visit (writer.go:213-217): hash, table, nearest earlier lane with the same hash
         if (prio & 1) __builtin_amdgcn_s_setprio(3);
         const uint32_t h = valid ? ((uint32_t)w0.hi * kHashMul) >> hsh : 0u;
-        const int32_t tv = valid ? (int32_t)hth[h] : 0;
-        const int32_t d = PredZ<G - 1>::get(valid ? h + 1 : 0u, 0);
-        const int32_t cand = valid ? (d ? x - d : tv) : 0;
+        int32_t cand = 0;
+        if (MSK) {
+            if (valid) cand = (int32_t)lds_mskor16(hth, h, (uint32_t)x);
+        } else {
+            const int32_t tv = valid ? (int32_t)hth[h] : 0;
+            const int32_t d = PredZ<G - 1>::get(valid ? h + 1 : 0u, 0);
+            cand = valid ? (d ? x - d : tv) : 0;
+        }
         V16 c0 = z0, c1 = z1;
         if (cand != 0) {
             if (kFwdCap == 20) bytes28(L, p, cand, c0, c1);
@@ -771,7 +794,11 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
             }
         }
         // ---- table: the visited lanes' positions (the last of a hash wins), then lane a's i+1
-        if (valid && (a < 0 || lj <= a)) hth[h] = (uint16_t)x;
+        if (MSK) {
+            if (valid && a >= 0 && lj > a && cand <= i + a) hth[h] = (uint16_t)cand;  // (visits Go never makes)
+        } else {
+            if (valid && (a < 0 || lj <= a)) hth[h] = (uint16_t)x;
+        }
         if (act && lj == a) {
             if (!rl && !zr && x + 1 + 4 <= n) hth[((uint32_t)(w0.hi >> 8) * kHashMul) >> hsh] = (uint16_t)(x + 1);
             if ((uint64_t)nrec < rcap) __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), rec + nrec);
@@ -1361,6 +1388,7 @@ constexpr int32_t kEdgeBefore = 64;  // readable bytes before a stream (WinRoll'
 __host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + kEdgeBefore + 64 + 15) & ~15ull; }
 __host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs &a) { return 128 + kEdgeSlots * edge_slot_bytes(a) + 16; }
 
+template <bool MSK>
 __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                  uint64_t rcap, int prio, uint8_t *edge) {
     constexpr int G = 16, S = 64 / G;
@@ -1405,7 +1433,7 @@ __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride
         __threadfence_block();
     }
     int32_t nrec = 0;
-    lean_loop(LeanIn{}, p, n, lj, g, hth, hsh, rec, rcap, prio, nrec, err);
+    lean_loop<MSK>(LeanIn{}, p, n, lj, g, hth, hsh, rec, rcap, prio, nrec, err);
     if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
 }
 
@@ -1630,9 +1658,12 @@ bool split_lean() {
 hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_lean, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
+    // the visit by one ds_mskor (when its lane order holds); EZ_K1S_MSK=0 takes the DPP search (A/B)
+    static const bool msk = knob("EZ_K1S_MSK", 1) != 0 && lds_mskor_in_lane_order();
     constexpr int S = 4;
     const uint32_t stride = split_stride<16, true>(a), tw = split_table_words<true>(a);
     const uint64_t rcap = rec_cap(a);
@@ -1644,7 +1675,10 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     if (z != hipSuccess) return z;
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
     static const size_t pad = (size_t)knob("EZ_K1S_LDSPAD", 0);
-    hipLaunchKernelGGL(k1_lean, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
+    if (msk)
+        hipLaunchKernelGGL(k1_lean<true>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
+    else
+        hipLaunchKernelGGL(k1_lean<false>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
@@ -1674,6 +1708,26 @@ __global__ void k_lds_store_order32(uint32_t *res) {
     t[l & 7] = l + 1;
     __syncthreads();
     if (l < 8 && t[l] != 56 + l + 1) atomicAdd(res, 1u);
+}
+
+// The property k1_lean<true> relies on, checked once per process on the device: same-word
+// ds_mskor_rtn_b32 of one wave instruction apply in ascending lane order (each lane reads the
+// entry as the latest earlier lane on it left it), on both halves of a word.
+__global__ void k_lds_mskor_order(uint32_t *res) {
+    __shared__ uint16_t t[8];
+    const uint32_t l = threadIdx.x;
+    if (l < 8) t[l] = 0;
+    __syncthreads();
+    const uint32_t e = (l * 5 + (l >> 3)) & 7;
+    const uint32_t got = lds_mskor16(t, e, l + 1);
+    uint32_t want = 0, last = 0;
+    for (uint32_t k = 0; k < 64; k++) {
+        const uint32_t ek = (k * 5 + (k >> 3)) & 7;
+        if (ek == e && k < l) want = k + 1;
+        if (l < 8 && ek == l) last = k + 1;
+    }
+    __syncthreads();
+    if (got != want || (l < 8 && t[l] != last)) atomicAdd(res, 1u);
 }
 
 // The property T32 relies on, checked once per process on the device: same-address LDS
@@ -1717,6 +1771,11 @@ bool lds_exchange_in_lane_order() {
 
 bool lds_store_in_lane_order() {
     static const bool ok = lds_probe(k_lds_store_order);
+    return ok;
+}
+
+bool lds_mskor_in_lane_order() {
+    static const bool ok = lds_probe(k_lds_mskor_order);
     return ok;
 }
 

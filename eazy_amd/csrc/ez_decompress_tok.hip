@@ -408,19 +408,71 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
             const int32_t need = D == 0 ? -0x7fffffff : cs + (D < L ? D : L);
             const int32_t ringlo = pos + total - R + 16;  // sources from here on are in the ring
             uint64_t cm = (EZ_EXP & 256) ? 0 : __ballot(cpy);
+            // ---- sources final at the round's start (every copy marked fre may run in any batch):
+            // zero regions, sources before the round, sources inside one literal of the round (all
+            // written above); a copy (D >= 16, not overlapping itself) whose source lies inside an
+            // earlier copy of the round reads that copy's source instead (the same bytes),
+            // repeated while it lands in a copy.  The token holding a position: the last lane whose
+            // output starts at or before it (dst is non-decreasing over the lanes; a lane with no
+            // output shares its dst with the next one)
+            int32_t ys = cs;  // the copy's (redirected) source
+            bool fre = cpy && (D == 0 || need <= pos);
+#if !(EZ_EXP & 8192)
+            if (cm) {
+                const int32_t tend = in ? dst + L : 0;
+                const int32_t tinf = !in ? 0 : (!tk.cp ? -1 : D);  // -1 literal, D > 0 a copy, 0 neither
+                int32_t ye = need;
+                bool open = cpy && !fre;
+                const bool redir = D >= 16 && D >= L;
+                // (two steps resolve 72 % of what any number would on C2's logs: a simulation of
+                // the rounds; each step a 4-way search, three dependent LDS round trips)
+                for (int it = 0; it < 2 && __ballot(open); it++) {
+                    const int32_t y = open ? ys : pos;
+                    int t = 0;
+#pragma unroll
+                    for (int st = 16; st > 0; st >>= 2) {
+                        const int32_t d1 = __builtin_amdgcn_ds_bpermute(4 * (t + st), dst);
+                        const int32_t d2 = __builtin_amdgcn_ds_bpermute(4 * (t + 2 * st), dst);
+                        const int32_t d3 = __builtin_amdgcn_ds_bpermute(4 * (t + 3 * st), dst);
+                        t += (d1 <= y ? st : 0) + (d2 <= y ? st : 0) + (d3 <= y ? st : 0);
+                    }
+                    const int32_t te = __builtin_amdgcn_ds_bpermute(4 * t, tend);
+                    const int32_t ti = __builtin_amdgcn_ds_bpermute(4 * t, tinf);
+                    if (open) {
+                        if (ys < pos || ye > te || t >= lane) {
+                            open = false;  // straddles tokens or the round's start: the batches decide
+                        } else if (ti < 0) {
+                            fre = true;  // inside a literal of the round
+                            open = false;
+                        } else if (ti > 0 && redir) {
+                            ys -= ti;
+                            ye -= ti;
+                            if (ye <= pos) {
+                                fre = true;
+                                open = false;
+                            }
+                        } else {
+                            open = false;
+                        }
+                    }
+                }
+                if (open) ys = cs;  // unresolved: the batches' rule, on the copy's own source
+            }
+#endif
             // a copy reading output flushed to HBM: the flush stores complete first (same CU: its
             // L1 then serves the bytes stored)
-            if (__ballot(cpy && D >= 16 && cs < ringlo)) __builtin_amdgcn_s_waitcnt(0);
+            if (__ballot(cpy && D >= 16 && ys < ringlo)) __builtin_amdgcn_s_waitcnt(0);
             while (cm) {
                 const int a = (int)__builtin_ctzll(cm);
                 const int32_t oa = __builtin_amdgcn_readlane(dst, a);
-                const uint64_t brk = __ballot(cpy && lane > a && need > oa);
+                const bool pend = (cm >> lane) & 1;
+                const uint64_t brk = __ballot(pend && !fre && lane > a && need > oa);
                 const int bnd = brk ? (int)__builtin_ctzll(brk) : kWave;
-                const bool ex = cpy && lane >= a && lane < bnd;
+                const bool ex = pend && (fre || lane < bnd);
                 // the common copy (D >= 16, source in the ring, after the stream start): 16-byte
                 // ring reads and exact writes; the others (runs and zero regions, sources before
                 // the start or past the ring) below
-                const bool slow = ex && (D < 16 || cs < 0 || cs < ringlo);
+                const bool slow = ex && (D < 16 || ys < 0 || ys < ringlo);
                 if (__ballot(slow)) {
                     V16 pv{0, 0};
                     int32_t stp = 16;
@@ -434,7 +486,7 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                         if (slow && o < L) {
                             V16 v = pv;  // a run's pattern; a zero region's zeros
                             if (D >= 16) {
-                                const int32_t x = cs + o;
+                                const int32_t x = ys + o;
                                 if (x >= ringlo) v = zero_before_start(rld<R>(ring, x), x);
                                 else v = far16(out, cap, b, x, nd, defs);  // flushed already (or deferred)
                             }
@@ -445,9 +497,9 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                 const bool fast = ex && !slow;
                 for (int32_t k = 0; __ballot(fast && 16 * k < L); k++) {
                     if (fast && 16 * k < L)
-                        rput_fast<R>(ring, dst + 16 * k, rld<R>(ring, cs + 16 * k), (uint32_t)(L - 16 * k < 16 ? L - 16 * k : 16), trash);
+                        rput_fast<R>(ring, dst + 16 * k, rld<R>(ring, ys + 16 * k), (uint32_t)(L - 16 * k < 16 ? L - 16 * k : 16), trash);
                 }
-                cm &= bnd >= kWave ? 0ull : ~((1ull << bnd) - 1);
+                cm &= ~__ballot(ex);
             }
             pos += total;
             t0 += nr;

@@ -292,3 +292,65 @@ def test_exactly_64k_streams_on_u16_tables(cuda):
     sparse[rng.random(65536) < 0.9] = 0
     bufs += [rng.integers(0, 256, 65536, dtype=np.uint8).tobytes(), sparse.tobytes(), bytes(65536), (b"abc" * 21846)[:65536]]
     _gpu_check(cuda, bufs, kinds=("", "S", "l", "w"))
+
+
+def _chain_stream(rng, n):
+    """Bytes built to make Reader.read's copies read each other within one K2t round: short
+    random literals, copies of a recent slice (often one that was itself a copy a few tokens
+    back), runs of period 1 - 40 right after a literal, overlapping copies with distance >= 16,
+    and zero stretches."""
+    b = bytearray(rng.integers(0, 256, 40, dtype=np.uint8).tobytes())
+    while len(b) < n:
+        k = int(rng.integers(0, 6))
+        if k == 0:
+            b += rng.integers(0, 256, int(rng.integers(1, 12)), dtype=np.uint8).tobytes()
+        elif k in (1, 2):  # a copy of a slice a little back
+            d = int(rng.integers(6, min(len(b), 300) + 1))
+            L = int(rng.integers(6, 60))
+            for _ in range(L):
+                b.append(b[-d])
+        elif k == 3:  # a run after a short literal
+            b += rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8).tobytes()
+            per = int(rng.integers(1, 41))
+            for _ in range(int(rng.integers(8, 90))):
+                b.append(b[-per])
+        elif k == 4:  # an overlapping copy with distance >= 16
+            d = min(int(rng.integers(16, 33)), len(b))
+            for _ in range(int(rng.integers(d + 1, 3 * d))):
+                b.append(b[-d])
+        else:
+            b += bytes(int(rng.integers(8, 64)))
+    return bytes(b[:n])
+
+
+@pytest.mark.gpu
+def test_k2t_copy_chains_within_rounds(cuda):
+    """K2t resolves, at each round's start, the copies whose sources are already final: inside
+    a literal of the round, or (distance >= 16, not overlapping) inside an earlier copy of the
+    round, whose own source they then read, repeatedly.  Streams made of such chains (and runs,
+    overlapping copies, zero stretches), 1 KiB - 300 KiB, every K2 decoder against the input,
+    statuses and sizes equal to the exact decoder's."""
+    import torch
+
+    import eazy_amd as ez
+
+    rng = np.random.default_rng(89)
+    lens = [1024, 4096, 5000, 20000, 65536, 70000, 300000] + [int(x) for x in rng.integers(2000, 40000, 25)]
+    bufs = [_chain_stream(rng, n) for n in lens]
+    want = [orc.compress(MiB, 1024, [b]) for b in bufs]
+    coff = np.concatenate([[0], np.cumsum([len(w) for w in want])]).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    comp = torch.from_numpy(np.frombuffer(b"".join(want) + bytes(64), np.uint8).copy()).to(cuda)
+    d_coff, d_offs = torch.from_numpy(coff).to(cuda), torch.from_numpy(offs).to(cuda)
+    _, sz0, st0 = ez.decompress_batch(comp, d_coff, d_offs, exact_only=True)
+    assert st0.abs().sum().item() == 0
+    for kind in ("t", "w", "r", ""):
+        ez.select_decompress_kernel(kind)
+        try:
+            out, sz, st = ez.decompress_batch(comp, d_coff, d_offs, max_len=max(lens))
+        finally:
+            ez.select_decompress_kernel("")
+        assert torch.equal(st, st0) and torch.equal(sz, sz0), kind
+        got = out[: int(offs[-1])].cpu().numpy().tobytes()
+        for s, b in enumerate(bufs):
+            assert got[offs[s] : offs[s + 1]] == b, f"K2 {kind!r}: stream {s} (len {lens[s]}) differs"
