@@ -680,9 +680,38 @@ __device__ __forceinline__ uint32_t lds_mskor16(uint16_t *hth, uint32_t h, uint3
     return (r >> sh) & 0xffffu;
 }
 
-template <bool MSK>
+// 12-bit entries, five to a 64-bit LDS word (streams of <= 4099 bytes: every position a table
+// holds is below 4096): 1,640 B per 1,024-entry table instead of 2,048, so 24 blocks of 4 streams fit
+// a CU's LDS instead of 20.  ds_mskor_rtn_b64 reads and sets one entry the way lds_mskor16 does.
+__device__ __forceinline__ void t12_at(uint32_t h, uint32_t &addr_off, uint32_t &sh) {
+    const uint32_t w = (h * 0x3334u) >> 16;  // h / 5 (h < 4096)
+    addr_off = w << 3;
+    sh = 12u * (h - 5u * w);
+}
+__device__ __forceinline__ uint32_t lds_mskor12(uint64_t *tab, uint32_t h, uint32_t val) {
+    uint32_t off, sh;
+    t12_at(h, off, sh);
+    const uint32_t addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t *)tab) + off;
+    const uint64_t m = 0xfffull << sh, v = (uint64_t)val << sh;
+    uint64_t r;
+    asm volatile("ds_mskor_rtn_b64 %0, %1, %2, %3\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(addr), "v"(m), "v"(v) : "memory");
+    return (uint32_t)(r >> sh) & 0xfffu;
+}
+// one entry set (no return: LDS operations of a wave complete in order, nothing waits for it)
+__device__ __forceinline__ void lds_put12(uint64_t *tab, uint32_t h, uint32_t val) {
+    uint32_t off, sh;
+    t12_at(h, off, sh);
+    const uint32_t addr = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) uint8_t *)tab) + off;
+    const uint64_t m = 0xfffull << sh, v = (uint64_t)val << sh;
+    asm volatile("ds_mskor_b64 %0, %1, %2" : : "v"(addr), "v"(m), "v"(v) : "memory");
+}
+
+// TB: the table's visit -- 0 the DPP search over a u16 table, 16 lds_mskor16, 12 lds_mskor12
+template <int TB>
 __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int32_t n, int lj, int g, uint16_t *hth,
-                                          uint32_t hsh, uint64_t *rec, uint64_t rcap, int prio, int32_t &nrec_out, int &err) {
+                                          uint32_t hsh, uint64_t *recw, uint32_t roff, uint64_t rcap, int prio, int32_t &nrec_out,
+                                          int &err) {
+    // (the records at recw + roff: recw is the wave's, in scalar registers, roff the group's)
     constexpr int G = 16;
     int32_t i = 0, done = 0, nrec = 0;
     bool live = !err && n >= 4;
@@ -708,7 +737,9 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         if (prio & 1) __builtin_amdgcn_s_setprio(3);
         const uint32_t h = valid ? ((uint32_t)w0.hi * kHashMul) >> hsh : 0u;
         int32_t cand = 0;
-        if (MSK) {
+        if (TB == 12) {
+            if (valid) cand = (int32_t)lds_mskor12((uint64_t *)hth, h, (uint32_t)x);
+        } else if (TB == 16) {
             if (valid) cand = (int32_t)lds_mskor16(hth, h, (uint32_t)x);
         } else {
             const int32_t tv = valid ? (int32_t)hth[h] : 0;
@@ -794,14 +825,24 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
             }
         }
         // ---- table: the visited lanes' positions (the last of a hash wins), then lane a's i+1
-        if (MSK) {
+        if (TB == 12) {
+            if (valid && a >= 0 && lj > a && cand <= i + a) lds_put12((uint64_t *)hth, h, (uint32_t)cand);
+        } else if (TB == 16) {
             if (valid && a >= 0 && lj > a && cand <= i + a) hth[h] = (uint16_t)cand;  // (visits Go never makes)
         } else {
             if (valid && (a < 0 || lj <= a)) hth[h] = (uint16_t)x;
         }
         if (act && lj == a) {
-            if (!rl && !zr && x + 1 + 4 <= n) hth[((uint32_t)(w0.hi >> 8) * kHashMul) >> hsh] = (uint16_t)(x + 1);
-            if ((uint64_t)nrec < rcap) __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), rec + nrec);
+            if (!rl && !zr && x + 1 + 4 <= n) {
+                const uint32_t h1 = ((uint32_t)(w0.hi >> 8) * kHashMul) >> hsh;
+                if (TB == 12) lds_put12((uint64_t *)hth, h1, (uint32_t)(x + 1));
+                else hth[h1] = (uint16_t)(x + 1);
+            }
+#if !(EZ_EXP & 32768)
+            if ((uint64_t)nrec < rcap) __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), recw + (roff + (uint32_t)nrec));
+#else  // (timing builds: the records' traffic without their lines -- k1_emit then sees none)
+            __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), recw + (roff + (uint32_t)(nrec & 1)));
+#endif
         }
         if (act) {
             if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
@@ -1388,8 +1429,8 @@ constexpr int32_t kEdgeBefore = 64;  // readable bytes before a stream (WinRoll'
 __host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + kEdgeBefore + 64 + 15) & ~15ull; }
 __host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs &a) { return 128 + kEdgeSlots * edge_slot_bytes(a) + 16; }
 
-template <bool MSK>
-__global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
+template <int TB>
+__global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                  uint64_t rcap, int prio, uint8_t *edge) {
     constexpr int G = 16, S = 64 / G;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1412,7 +1453,8 @@ __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride
     // group without a live stream never enters the loop and reads only the dummy region
     int err = !have || (uint64_t)n > A.max_len ? EZ_EINVAL : 0;
     const bool live = !err && n >= 4;
-    uint64_t *rec = recs + (have ? s * rcap : 0);
+    uint64_t *recw = recs + (uint64_t)blockIdx.x * S * rcap;  // (the wave's records; group g's at g * rcap)
+    const uint32_t roff = (uint32_t)(g * rcap);
     const uint8_t *p = live ? src : edge + 16;
     const bool edge_stream = live && (src - kEdgeBefore < blo || src + n + 64 > bhi);
     if (__ballot(edge_stream) != 0) {
@@ -1433,8 +1475,8 @@ __global__ __launch_bounds__(64, 5) void k1_lean(CompressArgs A, uint32_t stride
         __threadfence_block();
     }
     int32_t nrec = 0;
-    lean_loop<MSK>(LeanIn{}, p, n, lj, g, hth, hsh, rec, rcap, prio, nrec, err);
-    if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
+    lean_loop<TB>(LeanIn{}, p, n, lj, g, hth, hsh, recw, roff, rcap, prio, nrec, err);
+    if (have && lj == 0) A.out_size[s] = (uint64_t)((EZ_EXP & 32768) ? 0 : nrec) | ((uint64_t)err << 48);
 }
 
 // ---------------------------------------------------------------- K1e
@@ -1658,14 +1700,20 @@ bool split_lean() {
 hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_lean<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void *)k1_lean<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
-    // the visit by one ds_mskor (when its lane order holds); EZ_K1S_MSK=0 takes the DPP search (A/B)
+    // the visit by one ds_mskor (when its lane order holds); EZ_K1S_MSK=0 takes the DPP search (A/B).
+    // EZ_K1S_T12=1 (A/B) puts streams of <= 4099 bytes on 12-bit tables: 6 waves per SIMD instead of
+    // 5 measured the same at C1 (k1_lean 2,100 against 2,095 us), so the u16 tables stay
     static const bool msk = knob("EZ_K1S_MSK", 1) != 0 && lds_mskor_in_lane_order();
+    static const bool m12 = msk && knob("EZ_K1S_T12", 0) != 0 && lds_mskor64_in_lane_order();
+    const bool t12 = m12 && a.max_len <= 4099 && a.hs <= 4096;
     constexpr int S = 4;
-    const uint32_t stride = split_stride<16, true>(a), tw = split_table_words<true>(a);
+    const uint32_t w12 = (uint32_t)((2 * ((a.hs + 4) / 5) + 3) & ~3ll);  // u32 words of a 12-bit table
+    const uint32_t stride = t12 ? w12 : split_stride<16, true>(a), tw = t12 ? w12 : split_table_words<true>(a);
     const uint64_t rcap = rec_cap(a);
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
     static const int prio = knob("EZ_K1S_PRIO", 1);
@@ -1675,10 +1723,12 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     if (z != hipSuccess) return z;
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
     static const size_t pad = (size_t)knob("EZ_K1S_LDSPAD", 0);
-    if (msk)
-        hipLaunchKernelGGL(k1_lean<true>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
+    if (t12)
+        hipLaunchKernelGGL(k1_lean<12>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
+    else if (msk)
+        hipLaunchKernelGGL(k1_lean<16>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
     else
-        hipLaunchKernelGGL(k1_lean<false>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
+        hipLaunchKernelGGL(k1_lean<0>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
@@ -1710,7 +1760,7 @@ __global__ void k_lds_store_order32(uint32_t *res) {
     if (l < 8 && t[l] != 56 + l + 1) atomicAdd(res, 1u);
 }
 
-// The property k1_lean<true> relies on, checked once per process on the device: same-word
+// The property k1_lean<16> relies on, checked once per process on the device: same-word
 // ds_mskor_rtn_b32 of one wave instruction apply in ascending lane order (each lane reads the
 // entry as the latest earlier lane on it left it), on both halves of a word.
 __global__ void k_lds_mskor_order(uint32_t *res) {
@@ -1728,6 +1778,32 @@ __global__ void k_lds_mskor_order(uint32_t *res) {
     }
     __syncthreads();
     if (got != want || (l < 8 && t[l] != last)) atomicAdd(res, 1u);
+}
+
+// the same for ds_mskor_rtn_b64 on 12-bit fields (k1_lean<12>): five entries per word
+__global__ void k_lds_mskor64_order(uint32_t *res) {
+    __shared__ uint64_t t[2];
+    const uint32_t l = threadIdx.x;
+    if (l < 2) t[l] = 0;
+    __syncthreads();
+    const uint32_t e = (l * 7 + (l >> 3)) % 10;  // entries 0 - 9: both words, every field
+    const uint32_t got = lds_mskor12(t, e, l + 1);
+    uint32_t want = 0;
+    for (uint32_t k = 0; k < l; k++)
+        if ((k * 7 + (k >> 3)) % 10 == e) want = k + 1;
+    __syncthreads();
+    if (got != want) atomicAdd(res, 1u);
+    if (l < 10) {  // the final entries, and a put without return after them
+        uint32_t last = 0;
+        for (uint32_t k = 0; k < 64; k++)
+            if ((k * 7 + (k >> 3)) % 10 == l) last = k + 1;
+        const uint32_t sh = 12u * (l % 5);
+        if (((uint32_t)(t[l / 5] >> sh) & 0xfffu) != last) atomicAdd(res, 1u);
+    }
+    __syncthreads();
+    if (l < 10) lds_put12(t, l, 100 + l);
+    __syncthreads();
+    if (l < 10 && ((uint32_t)(t[l / 5] >> (12u * (l % 5))) & 0xfffu) != 100 + l) atomicAdd(res, 1u);
 }
 
 // The property T32 relies on, checked once per process on the device: same-address LDS
@@ -1776,6 +1852,11 @@ bool lds_store_in_lane_order() {
 
 bool lds_mskor_in_lane_order() {
     static const bool ok = lds_probe(k_lds_mskor_order);
+    return ok;
+}
+
+bool lds_mskor64_in_lane_order() {
+    static const bool ok = lds_probe(k_lds_mskor64_order);
     return ok;
 }
 

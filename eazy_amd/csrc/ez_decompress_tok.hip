@@ -418,7 +418,11 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
             int32_t ys = cs;  // the copy's (redirected) source
             bool fre = cpy && (D == 0 || need <= pos);
 #if !(EZ_EXP & 8192)
-            if (cm) {
+            // only in rounds with >= 16 copies reading the round's own output: there the searches
+            // pay (C4s: 26 -> 22 batches per round, K2 101 -> 94 ms); on C2's logs (10 such copies per
+            // round on average, 4.1 -> 3.0 batches) they cost more than the batches they save
+            // (4.44 -> 4.55 ms), and 2 % of its rounds reach 16
+            if (__builtin_popcountll(__ballot(cpy && !fre)) >= 16) {
                 const int32_t tend = in ? dst + L : 0;
                 const int32_t tinf = !in ? 0 : (!tk.cp ? -1 : D);  // -1 literal, D > 0 a copy, 0 neither
                 int32_t ye = need;

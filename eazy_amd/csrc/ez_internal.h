@@ -152,6 +152,7 @@ hipError_t launch_defer_copy(const DecompressArgs &a, hipStream_t s);       // K
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t s);   // K2t, token-parallel wave per stream
 bool lds_exchange_in_lane_order();  // the LDS property K1s-T32 relies on (checked once)
 bool lds_mskor_in_lane_order();     // the LDS property k1_lean's one-atomic visit relies on (checked once)
+bool lds_mskor64_in_lane_order();   // the same on 12-bit fields of 64-bit words (k1_lean<12>)
 hipError_t launch_pack(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes, uint64_t count,
                        uint8_t *packed, uint64_t *packed_off, void *workspace, hipStream_t s);
 size_t pack_workspace(uint64_t count);
