@@ -82,6 +82,8 @@ __global__ __launch_bounds__(kThreads) void k3_scan3(const uint64_t *sizes, uint
     }
 }
 
+typedef uint4 __attribute__((aligned(4))) uint4_a4;  // 16 bytes at a dword-aligned address
+
 __global__ __launch_bounds__(256) void k3_gather(const uint8_t *slots, const uint64_t *slot_off, const uint64_t *sizes,
                                                  uint64_t count, uint8_t *packed, const uint64_t *packed_off,
                                                  uint32_t split) {
@@ -109,10 +111,23 @@ __global__ __launch_bounds__(256) void k3_gather(const uint8_t *slots, const uin
         uint32_t *dw = (uint32_t *)(dst + head);
         // last source word index that holds a byte of this stream
         const uint64_t wlast = (r + (n - head) + 3) / 4 - 1;
-        for (uint64_t k = (uint64_t)j * kWave + lane; k < body; k += (uint64_t)split * kWave) {
-            const uint32_t w0 = sw[k];
-            const uint32_t w1 = sw[k + 1 <= wlast ? k + 1 : wlast];
-            dw[k] = __builtin_amdgcn_alignbyte(w1, w0, r);
+        // 16 bytes per lane and step (four dwords built from five source dwords; the source is read
+        // at dword granularity, never past its last word), the last < 4 dwords one at a time
+        const uint64_t body4 = body / 4;
+        for (uint64_t k = (uint64_t)j * kWave + lane; k < body4; k += (uint64_t)split * kWave) {
+            const uint64_t q = 4 * k;
+            const uint4 a = *(const uint4_a4 *)(sw + q);
+            const uint32_t e = sw[q + 4 <= wlast ? q + 4 : wlast];
+            *(uint4_a4 *)(dw + q) = make_uint4(__builtin_amdgcn_alignbyte(a.y, a.x, r), __builtin_amdgcn_alignbyte(a.z, a.y, r),
+                                              __builtin_amdgcn_alignbyte(a.w, a.z, r), __builtin_amdgcn_alignbyte(e, a.w, r));
+        }
+        if (j == 0) {
+            const uint64_t k = 4 * body4 + (uint64_t)lane;
+            if (k < body) {
+                const uint32_t w0 = sw[k];
+                const uint32_t w1 = sw[k + 1 <= wlast ? k + 1 : wlast];
+                dw[k] = __builtin_amdgcn_alignbyte(w1, w0, r);
+            }
         }
         const uint64_t t0 = head + body * 4;
         if (j == 0 && (uint64_t)lane < n - t0) dst[t0 + lane] = src[t0 + lane];
