@@ -218,6 +218,32 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
 #if (EZ_EXP & 2048)
         e = limr;
 #endif
+#if !(EZ_EXP & 1048576)
+        // exits two steps on, in place: the exit y of p, then the exit of y when y lies in the window
+        // and the chain through y leaves y's segment (no rare form on the way), else y -- the walk
+        // then crosses two segments per LDS round trip; the entries of the segments it steps over
+        // are filled in by the marking below (each is the exit of the segment before it)
+        {
+            uint32_t e2[8];
+            const uint4 r0 = *(const uint4 *)(ex + s0), r1 = *(const uint4 *)(ex + s0 + 8);
+            const uint32_t e1[8] = {r0.x, r0.y, r0.z, r0.w, r1.x, r1.y, r1.z, r1.w};
+#pragma unroll
+            for (int t = 0; t < 8; t++) {
+                uint32_t v = 0;
+#pragma unroll
+                for (int hh = 0; hh < 2; hh++) {
+                    const int32_t y = (int32_t)((e1[t] >> (16 * hh)) & 0xffffu);
+                    const int32_t z = y < limr ? (int32_t)ex[y] : y;
+                    v |= (uint32_t)(y < limr && z >= (y | 15) + 1 ? z : y) << (16 * hh);
+                }
+                e2[t] = v;
+            }
+            __syncthreads();  // (every lane has read the exits it needs)
+            *(uint4 *)(ex + s0) = make_uint4(e2[0], e2[1], e2[2], e2[3]);
+            *(uint4 *)(ex + s0 + 8) = make_uint4(e2[4], e2[5], e2[6], e2[7]);
+            __syncthreads();
+        }
+#endif
         while (e < limr) {  // (e, x, sl uniform)
             const int32_t sg = e >> 4;
             if (sg != sl) {
@@ -237,7 +263,8 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
         // ---- every lane marks the chain's token starts in its segment, from the entry
         const int32_t sm = se < limr ? se : limr;
         int32_t q2 = (int32_t)ent[lane];
-        q2 = q2 == 0xffff ? se : q2;
+        const bool had = q2 != 0xffff;
+        q2 = had ? q2 : se;
         uint32_t m16 = 0;
         while (__ballot(q2 < sm)) {
             if (q2 < sm) {
@@ -247,6 +274,25 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                 q2 += a;
             }
         }
+#if !(EZ_EXP & 1048576)
+        // the segments the walk stepped over: a marked segment's exit is the entry of the segment it
+        // lands in when that one has none yet (the chain's exits lie in distinct segments)
+        __syncthreads();
+        if (had && q2 < limr && ent[q2 >> 4] == 0xffff) ent[q2 >> 4] = (uint16_t)q2;
+        __syncthreads();
+        if (!had) {
+            q2 = (int32_t)ent[lane];
+            q2 = q2 == 0xffff ? se : q2;
+        }
+        while (__ballot(!had && q2 < sm)) {
+            if (!had && q2 < sm) {
+                m16 |= 1u << (q2 - s0);
+                int32_t a = (int32_t)tab[q2];
+                if (a == 0) a = (int32_t)ex[q2] - q2;
+                q2 += a;
+            }
+        }
+#endif
         // ---- the token list in input order: a wave prefix sum of the counts, then each lane's starts
         const int32_t mc = __builtin_popcount(m16);
         int32_t ic = mc;
