@@ -158,7 +158,9 @@ def load_traffic(path, workload, count, size, dom):
     # (k2_*) and the deferred-literal copy (kd_copy); K3 = k3_*; per step (a kernel a step runs several
     # times counts every dispatch)
     pre = {"k1_compress": ("k1_", "kx_"), "k2_decompress": ("k2_", "kd_"), "k3_pack": ("k3_",)}[dom]
-    vals = [v.get("per_step", v["traffic"]) for k, v in kern.items() if k.startswith(pre) and v.get("traffic")]
+    # (per_step is null in a profile without a k3_gather dispatch to count steps by: the per-launch figure)
+    vals = [v["per_step"] if v.get("per_step") is not None else v["traffic"] for k, v in kern.items()
+            if k.startswith(pre) and v.get("traffic")]
     src = os.path.relpath(path, ROOT) if path.startswith(ROOT) else path
     return (sum(vals) if vals else None), f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, {src}"
 

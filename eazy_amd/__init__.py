@@ -167,9 +167,17 @@ def select_compress_kernel(kind: str = "") -> None:
 
 
 def select_decompress_kernel(kind: str = "") -> None:
-    """Force the first K2 kernel of later batch decodes ('r' ring, 't' token-parallel wave per
-    stream, 'w' wave per stream; '' = automatic).  Tests and A/B measurement only."""
+    """Force the first K2 kernel of later batch decodes ('s' token walk + 16 lanes per stream,
+    slots <= 4 KiB; 'r' ring, 't' token-parallel wave per stream, 'w' wave per stream; '' =
+    automatic).  Tests and A/B measurement only."""
     _check(_lib().ez_select_decompress_kernel(ord(kind) if kind else 0))
+
+
+def decompress_kernel_last() -> str:
+    """The first K2 kernel the last batch decode of this process ran ('s', 'r', 't', 'w'; 'e'
+    the exact decoder alone; '' none yet)."""
+    v = _lib().ez_decompress_kernel_last()
+    return chr(v) if v else ""
 
 
 def _check(code: int, detail: int = 0) -> None:
@@ -299,15 +307,18 @@ class Writer:
         return len(p)
 
     def _failed(self, e: EazyError) -> EazyError:
-        """A device-side failure restarted the handle's stream: the mirror forgets w.b and
-        written too; an EZ_EINVAL carries the reference's panic value."""
-        self._resets += 1
-        if not _lib().ez_writer_is_reset(self._h):
-            _lib().ez_writer_reset(self._h)
-        self._b = bytearray()
-        self._written = 0
+        """A failed Write: when the device history had taken it, the handle restarted its stream
+        (it is reset now) and the mirror forgets w.b and written too; a failure found before
+        anything reached the device (ENOSPC, bad Write ends, no device) leaves both as they
+        were.  An EZ_EINVAL with a reference panic behind it carries that panic's value."""
+        if _lib().ez_writer_is_reset(self._h):
+            self._resets += 1
+            self._b = bytearray()
+            self._written = 0
         if isinstance(e, Panic):
-            return Panic(EINVAL, message=_lib().ez_panic_message(_lib().ez_writer_last_panic(self._h)).decode())
+            p = _lib().ez_writer_last_panic(self._h)
+            if p != 0:  # EZ_PANIC_NONE: an invalid argument, not a reference panic
+                return Panic(EINVAL, message=_lib().ez_panic_message(p).decode())
         return e
 
     def WriteBatch(self, ps) -> int:

@@ -20,6 +20,7 @@
 //   Decoder{Ver}.Tag/Offset/Meta                 eazy::Decoder                               reader.go:346-514
 //   error values ErrOverflow, ErrBreak, ...      eazy::Err (one code per value)              reader.go:57-76
 //   panics (bad sizes, impossible lengths)       eazy::Panic exception                        writer.go:162-168
+//   Dumper / NewDumper(w) / Dump(p)              eazy::Dumper / NewDumper / Dump              reader.go:43-54, 545-732
 //
 // The compute (Writer.Write's match-find/emit, Reader.Read's decode) runs in
 // the HIP kernels behind the C-ABI; with no usable GPU those calls fail with
@@ -32,7 +33,9 @@
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <memory>
+#include <tuple>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -201,11 +204,7 @@ class Writer {
         b_.resize(at + ez_compress_bound(n));
         const int st = ez_writer_write(h_, p, n, b_.data() + at, b_.size() - at, &got);
         b_.resize(at + (st == EZ_OK ? got : 0));
-        if (st != EZ_OK) {
-            failed();  // the handle restarted its stream: so does the mirror
-            detail::panic_if(st, ez_writer_last_panic(h_));
-            return {0, (Err)st};
-        }
+        if (st != EZ_OK) return {0, failed(st)};
         const Err e = write();
         if (e != Err::OK) return {0, e};
         return {n, Err::OK};
@@ -226,11 +225,7 @@ class Writer {
         std::vector<uint8_t> tmp(cap ? cap : 1);
         std::vector<uint64_t> oe(k);
         const int st = ez_writer_write_batch(h_, p, ends, k, tmp.data(), cap, oe.data());
-        if (st != EZ_OK) {
-            failed();
-            detail::panic_if(st, ez_writer_last_panic(h_));
-            return {0, (Err)st};
-        }
+        if (st != EZ_OK) return {0, failed(st)};
         const uint64_t gen = resets_;
         for (size_t j = 0, prev = 0; j < k; prev = oe[j], j++) {
             b_.insert(b_.end(), tmp.begin() + (ptrdiff_t)prev, tmp.begin() + (ptrdiff_t)oe[j]);
@@ -260,7 +255,9 @@ class Writer {
     void ResetSize(IoWriter *w, int64_t block, int64_t htable) {  // writer.go:155-159
         W = w;
         detail::size_panic(block, htable);
-        ez_writer_reset_size(h_, block, htable);
+        const int st = ez_writer_reset_size(h_, block, htable);
+        if (st != EZ_OK)  // (the sizes passed size_panic: a device failure; the handle keeps its old sizes)
+            throw std::runtime_error(std::string("eazy: ResetSize: ") + ez_strerror(st));
         b_.clear();
         written_ = 0;
     }
@@ -286,11 +283,22 @@ class Writer {
         if (st != EZ_OK) return (Err)st;
         return write();
     }
-    void failed() {  // a device-side failure: the handle is back at a fresh stream; forget w.b too
-        resets_++;
-        if (!ez_writer_is_reset(h_)) ez_writer_reset(h_);
-        b_.clear();
-        written_ = 0;
+    // A failed Write: when the device history had taken it, the handle restarted its stream (it is
+    // reset now) and the mirror forgets w.b and written too; a failure found before anything reached
+    // the device (NoSpace, bad Write ends, no device) leaves both as they were.  Invalid with a
+    // reference panic behind it throws that panic; without one it is an invalid argument.
+    Err failed(int st) {
+        if (ez_writer_is_reset(h_)) {
+            resets_++;
+            b_.clear();
+            written_ = 0;
+        }
+        if (st == EZ_EINVAL) {
+            const int p = ez_writer_last_panic(h_);
+            if (p != EZ_PANIC_NONE) throw Panic(ez_panic_message(p));
+            throw std::invalid_argument("eazy: Write: invalid arguments");
+        }
+        return (Err)st;
     }
     void reset() {  // writer.go:187-200
         resets_++;
@@ -408,12 +416,250 @@ inline std::unique_ptr<Reader> NewReaderBytes(const std::vector<uint8_t> &b, int
     return x;
 }
 
+// ---------------------------------------------------------------- Dumper (reader.go:43-54, 545-732)
+// The debug printer of a compressed stream, host side as in the reference: the tokens are walked
+// with the C-ABI's Decoder and printed one line each in the reference's text format (Go fmt verbs:
+// %x widths, %q quoting, % x).  Checked against eazy_amd/dump.py (tests/cpp/eazy_test.cpp).
+namespace detail {
+#include "eazy_isprint.inc"
+
+inline bool is_print(uint32_t r) {  // strconv.IsPrint as dump.py restates it
+    size_t lo = 0, hi = sizeof kPrintRanges / sizeof kPrintRanges[0];
+    while (lo < hi) {
+        const size_t m = (lo + hi) / 2;
+        if (r < kPrintRanges[m][0]) hi = m;
+        else if (r > kPrintRanges[m][1]) lo = m + 1;
+        else return true;
+    }
+    return false;
+}
+
+// utf8.DecodeRune of b[i..n): {rune, width}; {0xFFFD, 1} for an invalid encoding
+inline std::pair<uint32_t, int> decode_rune(const uint8_t *b, size_t n, size_t i) {
+    const uint32_t c = b[i];
+    if (c < 0x80) return {c, 1};
+    const int w = c >= 0xC2 && c <= 0xDF ? 2 : c >= 0xE0 && c <= 0xEF ? 3 : c >= 0xF0 && c <= 0xF4 ? 4 : 0;
+    if (w == 0 || i + (size_t)w > n) return {0xFFFD, 1};
+    // the second byte's range depends on the first (no overlongs, surrogates or > U+10FFFF)
+    const uint32_t c1 = b[i + 1];
+    const uint32_t lo = c == 0xE0 ? 0xA0 : c == 0xF0 ? 0x90 : 0x80, hi = c == 0xED ? 0x9F : c == 0xF4 ? 0x8F : 0xBF;
+    if (c1 < lo || c1 > hi) return {0xFFFD, 1};
+    uint32_t r = w == 2 ? (c & 0x1F) : w == 3 ? (c & 0x0F) : (c & 0x07);
+    r = (r << 6) | (c1 & 0x3F);
+    for (int k = 2; k < w; k++) {
+        const uint32_t ck = b[i + (size_t)k];
+        if (ck < 0x80 || ck > 0xBF) return {0xFFFD, 1};
+        r = (r << 6) | (ck & 0x3F);
+    }
+    return {r, w};
+}
+
+// fmt's %q of a []byte (strconv.Quote); *runes = its length in code points (fmt pads by those)
+inline std::string go_quote(const uint8_t *b, size_t n, size_t *runes = nullptr) {
+    std::string s = "\"";
+    size_t cnt = 1;
+    char esc[16];
+    for (size_t i = 0; i < n;) {
+        const auto [r, w] = decode_rune(b, n, i);
+        if (w == 1 && r == 0xFFFD) {
+            snprintf(esc, sizeof esc, "\\x%02x", b[i]);
+            s += esc;
+            cnt += 4;
+            i++;
+            continue;
+        }
+        const uint8_t *raw = b + i;
+        i += (size_t)w;
+        if (r == '"' || r == '\\') {
+            s += '\\';
+            s += (char)r;
+            cnt += 2;
+        } else if (is_print(r)) {
+            s.append((const char *)raw, (size_t)w);
+            cnt += 1;
+        } else if (r >= 7 && r <= 13) {  // \a \b \t \n \v \f \r
+            s += '\\';
+            s += "abtnvfr"[r - 7];
+            cnt += 2;
+        } else if (r < 0x20 || r == 0x7F) {
+            snprintf(esc, sizeof esc, "\\x%02x", r);
+            s += esc;
+            cnt += 4;
+        } else if (r < 0x10000) {
+            snprintf(esc, sizeof esc, "\\u%04x", r);
+            s += esc;
+            cnt += 6;
+        } else {
+            snprintf(esc, sizeof esc, "\\U%08x", r);
+            s += esc;
+            cnt += 10;
+        }
+    }
+    s += '"';
+    if (runes) *runes = cnt + 1;
+    return s;
+}
+
+inline void appendf(std::string &s, const char *fmt, long long a, long long b = 0) {
+    char t[64];
+    snprintf(t, sizeof t, fmt, a, b);
+    s += t;
+}
+}  // namespace detail
+
+class Dumper {
+  public:
+    IoWriter *W = nullptr;  // Dumper.Writer (nullptr: the text stays in Text())
+    // called once per printed item: input range, output offset, kind ('p','m','l','c','e'), length, offset
+    std::function<void(int64_t ioff, int64_t iend, int64_t ooff, uint8_t tag, int64_t l, int64_t off)> Debug;
+    int64_t GlobalOffset = 0;  // < 0: no global-offset column
+
+    // Dumper.Write reader.go:602-710: prints every whole token of p; {bytes those took, error}
+    std::pair<size_t, Err> Write(const uint8_t *p, size_t n) {
+        b_.clear();
+        size_t i = 0;
+        const Err e = walk(p, n, &i);
+        boff_ += (int64_t)i;
+        if (GlobalOffset >= 0) GlobalOffset += (int64_t)i;
+        Err out = e;
+        if (W) {
+            const Err we = W->Write((const uint8_t *)b_.data(), b_.size()).second;
+            if (out == Err::OK) out = we;
+        }
+        return {i, out};
+    }
+    std::pair<size_t, Err> Write(const std::vector<uint8_t> &p) { return Write(p.data(), p.size()); }
+
+    // Dumper.ReadFrom reader.go:563-600: a token cut by a read boundary is carried to the next read
+    std::pair<int64_t, Err> ReadFrom(IoReader *r) {
+        if (p_.empty()) p_.resize(0x10000);
+        size_t kept = 0;
+        int64_t total = 0;
+        Err err = Err::OK;
+        for (;;) {
+            size_t k;
+            std::tie(k, err) = r->Read(p_.data() + kept, p_.size() - kept);
+            if (k == 0) break;
+            total += (int64_t)k;
+            size_t used;
+            std::tie(used, err) = Write(p_.data(), kept + k);
+            std::memmove(p_.data(), p_.data() + used, kept + k - used);
+            kept = kept + k - used;
+            if (err != Err::OK && err != Err::ShortBuffer) break;
+        }
+        if (err == Err::EOF_) err = Err::OK;
+        if (kept != 0 && err == Err::OK) err = Err::UnexpectedEOF;
+        return {total, err};
+    }
+
+    Err Close() {  // reader.go:712-732
+        if (GlobalOffset >= 0) detail::appendf(b_, "%6llx  ", GlobalOffset);
+        detail::appendf(b_, "%4llx  %6llx  ", 0, pos_);
+        if (Debug) Debug(boff_, boff_, pos_, 'e', 0, 0);
+        return Err::OK;
+    }
+
+    const std::string &Text() const { return b_; }  // what the last Write / Close printed (d.b)
+
+  private:
+    int ver_ = 0;        // Decoder.Ver (a version meta sets it)
+    int64_t pos_ = 0;    // output position (r.pos)
+    int64_t boff_ = 0;   // input consumed by earlier Writes (r.boff)
+    std::string b_;
+    std::vector<uint8_t> p_;
+
+    void dbg(size_t st, size_t i, char kind, int64_t l, int64_t off) {
+        if (Debug) Debug(boff_ + (int64_t)st, boff_ + (int64_t)i, pos_, (uint8_t)kind, l, off);
+    }
+    Err walk(const uint8_t *p, size_t n, size_t *at) {
+        size_t i = 0;
+        for (;;) {
+            *at = i;
+            if (i >= n) return Err::OK;
+            const size_t st = i;
+            if (GlobalOffset >= 0) detail::appendf(b_, "%6llx  ", GlobalOffset + (long long)st);
+            detail::appendf(b_, "%4llx  %6llx  ", (long long)st, pos_);
+            while (i < n && p[i] == 0) i++;
+            if (i > st) {
+                detail::appendf(b_, "pad  %4llx\n", (long long)(i - st));
+                dbg(st, i, 'p', (int64_t)(i - st), 0);
+                continue;
+            }
+            int tag = 0;
+            int64_t l = 0;
+            size_t j = st;
+            Err e = (Err)ez_decode_tag(p, n, i, &tag, &l, &j);
+            if (e != Err::OK) return *at = st, e;
+            if (tag == Meta && l == 0) {
+                int64_t meta = 0, ml = 0;
+                size_t k = j;
+                e = (Err)ez_decode_meta(p, n, j, &meta, &ml, &k);
+                if (e != Err::OK) return *at = k, e;
+                if (k + (size_t)ml > n) return *at = k, Err::ShortBuffer;
+                if (meta == MetaVer && ml == 1) ver_ = p[k];
+                size_t runes = 0;
+                const std::string q = detail::go_quote(p + k, (size_t)ml, &runes);
+                detail::appendf(b_, "meta %2llx %llx  ", meta >> 3, ml);
+                b_ += q;
+                for (; runes < 8; runes++) b_ += ' ';
+                b_ += "  ";
+                for (int64_t x = 0; x < ml; x++) detail::appendf(b_, x ? " %02llx" : "%02llx", p[k + (size_t)x]);
+                b_ += '\n';
+                dbg(st, k, 'm', ml, meta);
+                i = k + (size_t)ml;
+            } else if (tag == Literal) {
+                if (j + (size_t)l > n) return *at = j, Err::ShortBuffer;
+                detail::appendf(b_, "lit  %4llx        ", l);
+                b_ += detail::go_quote(p + j, (size_t)l);
+                b_ += '\n';
+                dbg(st, j, 'l', l, 0);
+                i = j + (size_t)l;
+                pos_ += l;
+            } else {  // Copy
+                const bool lng = j < n && p[j] == OffLong;
+                int64_t off = 0;
+                size_t k = j;
+                e = (Err)ez_decode_offset(p, n, j, l, &off, &k);
+                if (e != Err::OK) return *at = st, e;
+                detail::appendf(b_, "copy %4llx  off %4llx", l, off);
+                if (lng) b_ += "  (long)";
+                b_ += '\n';
+                dbg(st, k, 'c', l, off);
+                i = k;
+                pos_ += l;
+            }
+        }
+    }
+};
+
+inline std::unique_ptr<Dumper> NewDumper(IoWriter *w) {  // reader.go:557-561
+    auto d = std::make_unique<Dumper>();
+    d->W = w;
+    return d;
+}
+
+// Dump reader.go:545-555: the debug print of a compressed buffer, with the error that stopped it
+inline std::string Dump(const uint8_t *p, size_t n) {
+    Dumper d;
+    const Err e = d.Write(p, n).second;
+    d.Close();
+    std::string s = d.Text();
+    if (e != Err::OK) s += "\nerror: " + ErrorText(e);
+    return s;
+}
+inline std::string Dump(const std::vector<uint8_t> &p) { return Dump(p.data(), p.size()); }
+
 // ---------------------------------------------------------------- batches (the GPU hot path)
 // One stream per buffer = a fresh NewWriter(block, htable) receiving one
 // Write; device pointers, asynchronous on `hip_stream`.  See include/eazy.h.
+// Invalid sizes throw the reference's Panic (Writer.init); other invalid batch arguments throw
+// std::invalid_argument (Err::Invalid is never returned).
 inline Err CompressBatch(int64_t block, int64_t htable, bool append_magic, const ez_batch &b, void *hip_stream) {
     const int st = ez_compress_batch(block, htable, append_magic ? 0 : EZ_F_NO_MAGIC, &b, hip_stream);
-    if (st == EZ_EINVAL) detail::size_panic(block, htable);
+    if (st == EZ_EINVAL) {
+        detail::size_panic(block, htable);
+        throw std::invalid_argument("eazy: CompressBatch: invalid batch arguments");
+    }
     return (Err)st;
 }
 inline Err DecompressBatch(int64_t block_size_limit, const ez_batch &b, void *workspace, void *hip_stream) {

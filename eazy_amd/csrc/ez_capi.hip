@@ -439,6 +439,7 @@ int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t
 }
 
 int writer_run(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, uint8_t *out, size_t cap, uint64_t *out_ends) {
+    w->last_panic = EZ_PANIC_NONE;  // (set again only by a failure of this call)
     const size_t n = k ? (size_t)ends[k - 1] : 0;
     size_t bound = 0;
     for (size_t j = 0; j < k; j++) {
@@ -819,10 +820,12 @@ extern "C" int ez_select_compress_kernel(int kind) {
 }
 
 extern "C" int ez_select_decompress_kernel(int kind) {
-    if (kind != 0 && kind != 'r' && kind != 'w' && kind != 't') return EZ_EINVAL;
+    if (kind != 0 && kind != 's' && kind != 'r' && kind != 'w' && kind != 't') return EZ_EINVAL;
     ez::select_decompress_variant(kind);
     return EZ_OK;
 }
+
+extern "C" int ez_decompress_kernel_last(void) { return ez::last_decompress_variant(); }
 
 extern "C" size_t ez_decompress_workspace(uint64_t count) {
     return (size_t)ez::decompress_workspace_words(count) * sizeof(uint32_t);

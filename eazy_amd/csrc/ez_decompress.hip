@@ -236,46 +236,99 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
 
 }  // namespace
 
-// the batch decoders: K2r (lane per stream, slots < 64 KiB) or K2t (token-parallel wave per
-// stream, longer slots), each handing the streams it does not finish to the exact decoder; 'r',
-// 't' / 'w' force one (tests, A/B; K2w is reached only this way)
-static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'r', 't', 'w'
+// the batch decoders: K2s (slots of at most 4 KiB: a token-walk kernel and a move kernel), K2r
+// (lane per stream, slots < 64 KiB) or K2t (token-parallel wave per stream, longer slots), each
+// handing the streams it does not finish to the exact decoder; 's', 'r', 't' / 'w' force one
+// (tests, A/B; K2w is reached only this way)
+static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 's', 'r', 't', 'w'
 void select_decompress_variant(int v) { g_decompress_variant = v; }
+static int g_last_variant = 0;  // the first K2 kernel of the last batch decode ('e': exact alone)
+int last_decompress_variant() { return g_last_variant; }
 
-// [slow list: 2 * count + 32 words][K2w's deferred literals: 4 words + count * kDefSlots records]
+// [slow list: 2 * count + 32 words][K2w / K2t's deferred literals: 4 words + count * kDefSlots
+// records, or K2s's per-stream token bitmaps: count * kSmallRegion words (one or the other)]
 uint64_t decompress_workspace_words(uint64_t count) {
-    return 2 * count + 32 + 4 + count * (uint64_t)kDefSlots * (sizeof(DeferLit) / 4);
+    const uint64_t defer = 4 + count * (uint64_t)kDefSlots * (sizeof(DeferLit) / 4);
+    const uint64_t small = count * (uint64_t)kSmallRegion;
+    return 2 * count + 32 + (defer > small ? defer : small);
 }
 
-hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
-    if (a.count == 0) return hipSuccess;
-    if (a.handle || !a.slow) {
-        uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);
-        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+namespace {
+// the largest output slot of a batch (saturated at 2^32 - 1) into *mx
+__global__ void k_max_slot(const uint64_t *out_off, uint64_t count, uint32_t *mx) {
+    uint64_t m = 0;
+    for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < count; s += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t d = out_off[s + 1] - out_off[s];
+        m = d > m ? d : m;
+    }
+    atomicMax(mx, (uint32_t)(m > 0xffffffffull ? 0xffffffffull : m));
+}
+}  // namespace
+
+// The decoder a batch takes depends on its largest output slot: the caller's hint (ez_batch.max_len)
+// when given, else measured here (one small kernel and a 4-byte read back, which waits for the stream).
+static hipError_t largest_slot(const DecompressArgs &a, hipStream_t st, uint64_t *mo) {
+    if (a.max_out != 0) {
+        *mo = a.max_out;
+        return hipSuccess;
+    }
+    uint32_t *mx = a.slow + 2 * a.count + 31;  // (the slow list's spare words)
+    hipError_t e = hipMemsetAsync(mx, 0, sizeof(uint32_t), st);
+    if (e != hipSuccess) return e;
+    const uint64_t blocks = (a.count + 255) / 256;
+    hipLaunchKernelGGL(k_max_slot, dim3((unsigned)(blocks < 1024 ? blocks : 1024)), dim3(256), 0, st, a.out_off, a.count, mx);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    uint32_t h = 0;
+    if ((e = hipMemcpyAsync(&h, mx, sizeof h, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    *mo = h;
+    return hipSuccess;
+}
+
+hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
+    if (a0.count == 0) return hipSuccess;
+    if (a0.handle || !a0.slow) {
+        if (!a0.handle) g_last_variant = 'e';
+        uint64_t grid = a0.count < (1u << 30) ? a0.count : (1u << 30);
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a0);
         return hipGetLastError();
     }
     // EZ_K2=exact (experiments): the exact decoder alone
     static const bool use_exact = knob_str("EZ_K2") && strcmp(knob_str("EZ_K2"), "exact") == 0;
     static const uint64_t long_slot = (uint64_t)knob("EZ_K2_LONG", 64 << 10);
     if (use_exact) {
-        DecompressArgs b = a;
+        g_last_variant = 'e';
+        DecompressArgs b = a0;
         b.slow = nullptr;
         uint64_t grid = b.count < (1u << 30) ? b.count : (1u << 30);
         hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, b);
         return hipGetLastError();
     }
-    hipError_t e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st);
+    DecompressArgs a = a0;
+    hipError_t e = largest_slot(a0, st, &a.max_out);
     if (e != hipSuccess) return e;
+    if ((e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st)) != hipSuccess) return e;
     if (g_decompress_variant < 0) {
         const char *v = knob_str("EZ_K2");
-        g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w' : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : 0));
+        g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w'
+                               : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : (v && strcmp(v, "small") == 0 ? 's' : 0)));
     }
-    // Slots of 64 KiB and more (C2, C4, the sweep's long streams) go to K2t; shorter ones to K2r's lane
-    // per stream (1 GiB batches, K2 ms, K2r / K2t: 8 KiB 1.89 / 4.99, 16 KiB 1.96 / 4.89, 32 KiB 3.50 /
-    // 5.06, 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5) - / 7.0, 1 MiB (K2w 29.7) -
-    // / 14.4; C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms)
-    const bool long_slots = a.max_out >= long_slot;
-    if (g_decompress_variant == 't' || (g_decompress_variant == 0 && long_slots)) {
+    const uint64_t exact_grid = a.count < 4096 ? a.count : 4096;
+    // Slots of at most 4 KiB (C1, C3) go to K2s; up to 64 KiB to K2r's lane per stream; longer ones (C2,
+    // C4, the sweep's long streams) to K2t (1 GiB batches, K2 ms, K2r / K2t: 8 KiB 1.89 / 4.99, 16 KiB
+    // 1.96 / 4.89, 32 KiB 3.50 / 5.06, 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5)
+    // - / 7.0, 1 MiB (K2w 29.7) - / 14.4; C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms)
+    const int v = g_decompress_variant != 0 ? g_decompress_variant : (a.max_out <= (uint64_t)kSmallOut ? 's' : (a.max_out >= long_slot ? 't' : 'r'));
+    g_last_variant = v;
+    if (v == 's') {
+        // K2s: the token walk writes each stream's bitmap of token starts (or hands it over), the move
+        // kernel decodes the streams the walk took
+        e = launch_decompress_small(a, a.slow + 2 * a.count + 32, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)exact_grid), dim3(64), 0, st, a);
+        return hipGetLastError();
+    }
+    if (v == 't') {
         // K2t: token-parallel, a wave per stream; its hand-overs go to the exact decoder, the long
         // literals it defers are moved last (the exact decoder writes the same bytes for a stream it takes)
         DecompressArgs b = a;
@@ -287,14 +340,13 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
 #if (EZ_EXP & 4096)
         return e;  // debug builds: the hand-over codes stay in the statuses
 #endif
-        const uint64_t grid = a.count < 4096 ? a.count : 4096;
-        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)exact_grid), dim3(64), 0, st, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         return launch_defer_copy(b, st);
     }
-    if (g_decompress_variant == 'w') {
-        // K2w (forced: tests, A/B): a wave per stream with a scalar token walk; its hand-overs go to
-        // the exact decoder; the long literals it defers are moved last
+    if (v == 'w') {
+        // K2w (forced: tests, A/B): a wave per stream with a scalar token walk; its hand-overs go to the
+        // exact decoder; the long literals it defers are moved last
         DecompressArgs b = a;
         static const bool no_defer = knob("EZ_K2W_DEFER", 1) == 0;  // A/B
         b.defer = no_defer ? nullptr : a.slow + 2 * a.count + 32;
@@ -302,16 +354,14 @@ hipError_t launch_decompress(const DecompressArgs &a, hipStream_t st) {
         if (b.defer && (e = hipMemsetAsync(b.defer, 0, 16, st)) != hipSuccess) return e;
         e = launch_decompress_wave(b, st);
         if (e != hipSuccess) return e;
-        const uint64_t grid = a.count < 4096 ? a.count : 4096;
-        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)exact_grid), dim3(64), 0, st, a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         return b.defer ? launch_defer_copy(b, st) : hipSuccess;
     }
-    // K2r (default): one lane per stream with the recent output in an LDS ring
+    // K2r: one lane per stream with the recent output in an LDS ring
     e = launch_decompress_ring(a, st);
     if (e != hipSuccess) return e;
-    const uint64_t grid = a.count < 4096 ? a.count : 4096;
-    hipLaunchKernelGGL(k2_decompress, dim3((unsigned)grid), dim3(64), 0, st, a);
+    hipLaunchKernelGGL(k2_decompress, dim3((unsigned)exact_grid), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

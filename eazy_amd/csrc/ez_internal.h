@@ -145,11 +145,18 @@ hipError_t launch_general(const CompressArgs &a, hipStream_t s);
 uint64_t compress_scratch_words(const CompressArgs &a);
 hipError_t launch_decompress(const DecompressArgs &a, hipStream_t s);
 void select_decompress_variant(int v);
+int last_decompress_variant();  // the first K2 kernel of the last batch decode
 // K2r: one lane per stream with a 512-byte LDS ring of recent output (ez_decompress_ring.hip)
 hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t s);
 hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t s);  // K2w, long streams
 hipError_t launch_defer_copy(const DecompressArgs &a, hipStream_t s);       // K2w's deferred literals
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t s);   // K2t, token-parallel wave per stream
+// K2s: small streams (slots <= kSmallOut), a token-walk kernel (lane per stream) writing a bitmap of
+// token starts into bm (kSmallRegion words per stream), then a move kernel (16 lanes per stream)
+constexpr int32_t kSmallOut = 4096;                 // output slots K2s takes
+constexpr int32_t kSmallIn = 6144;                  // compressed streams K2s takes (>= ez_compress_bound(4096))
+constexpr uint32_t kSmallRegion = 1 + kSmallIn / 32;  // [token count | hand over][one bit per input byte]
+hipError_t launch_decompress_small(const DecompressArgs &a, uint32_t *bm, hipStream_t s);
 bool lds_exchange_in_lane_order();  // the LDS property K1s-T32 relies on (checked once)
 bool lds_mskor_in_lane_order();     // the LDS property k1_lean's one-atomic visit relies on (checked once)
 bool lds_mskor64_in_lane_order();   // the same on 12-bit fields of 64-bit words (k1_lean<12>)

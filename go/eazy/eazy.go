@@ -23,6 +23,7 @@ import (
 	"errors"
 	"fmt"
 	"io"
+	"runtime"
 	"unsafe"
 )
 
@@ -150,19 +151,39 @@ type Writer struct {
 	ver     int
 }
 
+// Device is the HIP device NewWriter and NewReader put their handles on (no
+// reference counterpart: the reference runs on the host).  Set it before
+// creating handles, or use NewWriterOn / NewReaderOn.
+var Device = 0
+
 // NewWriter creates a new Writer (writer.go:133-145).  block and htable are
 // powers of two; block is the window size, htable the hash table entries.
 func NewWriter(wr io.Writer, block, htable int) *Writer {
+	return NewWriterOn(wr, block, htable, Device)
+}
+
+// NewWriterOn is NewWriter with the handle on HIP device dev.
+func NewWriterOn(wr io.Writer, block, htable, dev int) *Writer {
 	sizePanic(block, htable)
 	w := &Writer{Writer: wr, AppendMagic: true}
-	if st := C.ez_writer_new(C.int64_t(block), C.int64_t(htable), 0, &w.h); st != C.EZ_OK {
+	if st := C.ez_writer_new(C.int64_t(block), C.int64_t(htable), C.int(dev), &w.h); st != C.EZ_OK {
 		panic(toErr(st, 0))
 	}
+	// The reference Writer has nothing to release, so drop-in callers never Close:
+	// the handle's device ring, table, HIP stream and pinned buffer go with the Writer.
+	runtime.SetFinalizer(w, (*Writer).Close)
 	return w
 }
 
-// Close releases the device state (the reference has nothing to release).
-func (w *Writer) Close() { C.ez_writer_free(w.h); w.h = nil }
+// Close releases the device state now (the reference has nothing to release; a
+// Writer that is never closed releases it when it is garbage collected).
+func (w *Writer) Close() {
+	if w.h != nil {
+		C.ez_writer_free(w.h)
+		w.h = nil
+	}
+	runtime.SetFinalizer(w, nil)
+}
 
 func (w *Writer) sync() {
 	m := 0
@@ -186,6 +207,7 @@ func (w *Writer) Write(p []byte) (int, error) {
 	out := w.b[at : at+need]
 	var n C.size_t
 	st := C.ez_writer_write(w.h, ptr(p), C.size_t(len(p)), ptr(out), C.size_t(need), &n)
+	runtime.KeepAlive(w)
 	if st != C.EZ_OK {
 		return 0, w.failed(st)
 	}
@@ -244,17 +266,21 @@ func (w *Writer) ResetSize(wr io.Writer, block, htable int) {
 
 func (w *Writer) reset() { w.resets++; C.ez_writer_reset(w.h); w.b = w.b[:0]; w.written = 0 }
 
-// failed: a device-side failure restarted the handle's stream; the mirror forgets w.b and
-// written with it, and an EZ_EINVAL re-panics with the reference's value.
+// failed: when the device history had taken the Write, the handle restarted its stream
+// (it is reset now) and the mirror forgets w.b and written with it; a failure found before
+// anything reached the device (no space, bad Write ends, no device) leaves both as they were.
+// An EZ_EINVAL with a reference panic behind it re-panics with that value.
 func (w *Writer) failed(st C.int) error {
-	w.resets++
-	if C.ez_writer_is_reset(w.h) == 0 {
-		C.ez_writer_reset(w.h)
+	if C.ez_writer_is_reset(w.h) != 0 {
+		w.resets++
+		w.b = w.b[:0]
+		w.written = 0
 	}
-	w.b = w.b[:0]
-	w.written = 0
 	if st == C.EZ_EINVAL {
-		panic(panicValue(C.ez_writer_last_panic(w.h), 0))
+		if p := C.ez_writer_last_panic(w.h); p != C.EZ_PANIC_NONE {
+			panic(panicValue(p, 0))
+		}
+		return errors.New("eazy: invalid Write arguments")
 	}
 	return toErr(st, 0)
 }
@@ -280,6 +306,7 @@ func (w *Writer) WriteBatch(ps [][]byte) (int, error) {
 	oe := make([]uint64, len(ps))
 	st := C.ez_writer_write_batch(w.h, ptr(data), (*C.uint64_t)(unsafe.Pointer(&ends[0])), C.size_t(len(ps)),
 		ptr(out), C.size_t(need), (*C.uint64_t)(unsafe.Pointer(&oe[0])))
+	runtime.KeepAlive(w)
 	if st != C.EZ_OK {
 		return 0, w.failed(st)
 	}
@@ -343,28 +370,40 @@ type Reader struct {
 }
 
 // NewReader creates a Reader over rd (reader.go:79-86).
-func NewReader(rd io.Reader) *Reader {
+func NewReader(rd io.Reader) *Reader { return NewReaderOn(rd, Device) }
+
+// NewReaderOn is NewReader with the handle on HIP device dev.
+func NewReaderOn(rd io.Reader, dev int) *Reader {
 	r := &Reader{Reader: rd, BlockSizeLimit: 16 * MiB, BufferSize: 64 * KiB}
-	r.open()
+	r.open(dev)
 	return r
 }
 
 // NewReaderBytes creates a Reader over b (reader.go:89-94).
 func NewReaderBytes(b []byte) *Reader {
 	r := &Reader{}
-	r.open()
+	r.open(Device)
 	r.ResetBytes(b)
 	return r
 }
 
-func (r *Reader) open() {
-	if st := C.ez_reader_new(0, &r.h); st != C.EZ_OK {
+func (r *Reader) open(dev int) {
+	if st := C.ez_reader_new(C.int(dev), &r.h); st != C.EZ_OK {
 		panic(toErr(st, 0))
 	}
+	// as for Writer: drop-in callers never Close, the handle goes with the Reader
+	runtime.SetFinalizer(r, (*Reader).Close)
 }
 
-// Close releases the device state.
-func (r *Reader) Close() { C.ez_reader_free(r.h); r.h = nil }
+// Close releases the device state now (a Reader that is never closed releases it
+// when it is garbage collected).
+func (r *Reader) Close() {
+	if r.h != nil {
+		C.ez_reader_free(r.h)
+		r.h = nil
+	}
+	runtime.SetFinalizer(r, nil)
+}
 
 // Reset restarts decoding from rd (reader.go:96-99).
 func (r *Reader) Reset(rd io.Reader) { r.ResetBytes(nil); r.Reader = rd }
@@ -393,6 +432,7 @@ func (r *Reader) Read(p []byte) (n int, err error) {
 		var det C.int64_t
 		st := C.ez_reader_read(r.h, ptr(r.b), C.size_t(len(r.b)), C.size_t(r.i), C.int64_t(r.boff),
 			ptr(p[n:]), C.size_t(len(p)-n), &m, &i, &det)
+		runtime.KeepAlive(r)
 		n += int(m)
 		r.i = int(i)
 		if n == len(p) {

@@ -213,10 +213,16 @@ int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t
  * back to the automatic choice.  Not thread-safe against concurrent calls. */
 int ez_select_compress_kernel(int kind);
 /* Testing / A-B measurement: the first K2 kernel of later batch decodes with a
- * workspace ('r' lane-per-stream with an LDS ring of recent output, 't' token-parallel wave per
- * stream, 'w' wave per stream with a scalar token walk; 0 = automatic: 't' for slots of 64 KiB
- * and more, else 'r').  Streams either cannot take go on to the exact decoder. */
+ * workspace ('s' a token-walk kernel then 16 lanes per stream with the whole output in LDS, for
+ * slots of at most 4 KiB; 'r' lane-per-stream with an LDS ring of recent output, 't'
+ * token-parallel wave per stream, 'w' wave per stream with a scalar token walk; 0 = automatic:
+ * 's' when every slot is at most 4 KiB, 't' when one is 64 KiB or more, else 'r'; the largest
+ * slot is max_len when the caller gives it, else measured on the device, which waits for the
+ * stream).  Streams the chosen kernel cannot take go on to the exact decoder. */
 int ez_select_decompress_kernel(int kind);
+/* Introspection: the first K2 kernel the last ez_decompress_batch call of this process ran ('s',
+ * 'r', 't', 'w'; 'e' the exact decoder alone; 0 none yet). */
+int ez_decompress_kernel_last(void);
 
 #ifdef __cplusplus
 }

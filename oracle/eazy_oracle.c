@@ -903,13 +903,19 @@ static void *batch_worker(void *arg) {
     return NULL;
 }
 
+/* streams handed out in grains of at most 64, and small enough that every
+   thread gets work (a batch of 64 long streams spreads over all threads) */
+int64_t or_batch_grain(int64_t count, int nthreads) {
+    if (nthreads < 1) nthreads = 1;
+    int64_t g = count / ((int64_t)nthreads * 4);
+    if (g > 64) g = 64;
+    if (g < 1) g = 1;
+    return g;
+}
+
 static int run_batch(batch_job *j, int nthreads) {
     if (nthreads < 1) nthreads = 1;
-    /* streams handed out in grains of at most 64, and small enough that every
-       thread gets work (a batch of 64 long streams spreads over all threads) */
-    j->grain = j->count / ((int64_t)nthreads * 4);
-    if (j->grain > 64) j->grain = 64;
-    if (j->grain < 1) j->grain = 1;
+    j->grain = or_batch_grain(j->count, nthreads);
     pthread_mutex_init(&j->mu, NULL);
     pthread_t *t = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nthreads);
     for (int k = 0; k < nthreads; k++) pthread_create(&t[k], NULL, batch_worker, j);

@@ -101,6 +101,8 @@ int or_compress(int64_t block, int64_t htable, int append_magic, int ver, const 
 int or_decompress(const uint8_t *in, int64_t n, int64_t buf_size, uint8_t *out, int64_t cap,
                   int64_t *out_len, int64_t *breaks);
 /* Independent streams, one Write each, spread over nthreads host threads. */
+/* the number of streams one batch task takes (count / (4 * threads), clamped to [1, 64]) */
+int64_t or_batch_grain(int64_t count, int nthreads);
 int or_compress_batch(int64_t block, int64_t htable, const uint8_t *in, const int64_t *in_off,
                       int64_t count, uint8_t *slots, const int64_t *slot_off, int64_t *sizes,
                       int nthreads);

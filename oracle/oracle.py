@@ -69,6 +69,8 @@ def lib():
         L.or_reader_detail.argtypes = [C.c_void_p]
         L.or_compress.argtypes = [_i64, _i64, C.c_int, C.c_int, C.c_char_p, _i64p, C.c_int, C.c_void_p, _i64, _i64p]
         L.or_decompress.argtypes = [C.c_char_p, _i64, _i64, C.c_void_p, _i64, _i64p, _i64p]
+        L.or_batch_grain.restype = _i64
+        L.or_batch_grain.argtypes = [_i64, C.c_int]
         L.or_compress_batch.argtypes = [_i64, _i64, C.c_void_p, C.c_void_p, _i64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         L.or_decompress_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, _i64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
         for name in ("or_enc_tag", "or_enc_offset", "or_enc_meta"):
@@ -241,6 +243,11 @@ def decompress(b: bytes, buf_size: int = 1 << 16, cap: int | None = None):
 
 def _ptr(a: np.ndarray):
     return a.ctypes.data_as(C.c_void_p)
+
+
+def batch_grain(count: int, nthreads: int) -> int:
+    """Streams per task of the threaded batch runners."""
+    return int(lib().or_batch_grain(count, nthreads))
 
 
 def compress_batch(block, htable, data: np.ndarray, offs: np.ndarray, slot_offs: np.ndarray, nthreads: int):

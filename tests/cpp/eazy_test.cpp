@@ -8,6 +8,8 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
@@ -474,7 +476,125 @@ static void TestWriteBatch() {  // Writer::WriteBatch == Write on each in turn (
     }
 }
 
+// Handles that are created and dropped give their device memory back: a drop-in caller never
+// closes a Writer or Reader (the reference has nothing to close), so the destructor must free
+// the ring, the table, the HIP stream and the staging buffers.
+static size_t device_free() {
+    size_t fr = 0, tot = 0;
+    CHECK(hipMemGetInfo(&fr, &tot) == hipSuccess);
+    return fr;
+}
+static void TestHandleLeak() {
+    Bytes p;
+    for (int k = 0; k < 4096; k++) p.push_back((uint8_t)("ts=2 level=info msg=\"ok\" "[(k * 5) % 27]));
+    {  // warm: the first handles initialise the runtime and the kernels' one-time probes
+        Buffer buf;
+        auto w = NewWriter(&buf, MiB, 1024);
+        write_ok(*w, p);
+        auto r = NewReaderBytes(buf.b);
+        (void)r->Read(p.size());
+    }
+    CHECK(hipDeviceSynchronize() == hipSuccess);
+    const size_t base = device_free();
+    for (int round = 0; round < 64; round++) {
+        Buffer buf;
+        auto w = NewWriter(&buf, 4 * MiB, 4096);  // a 4 MiB ring and a 16 KiB table per handle
+        write_ok(*w, p);
+        auto r = NewReaderBytes(buf.b);
+        auto [out, e] = r->Read(p.size());
+        CHECK(out == p);
+    }
+    CHECK(hipDeviceSynchronize() == hipSuccess);
+    const size_t after = device_free();
+    // 64 leaked Writers would hold >= 256 MiB; allow the allocator's slack (a few MiB)
+    std::printf("    device free: %zu -> %zu MiB\n", base >> 20, after >> 20);
+    CHECK(after + (16u << 20) >= base);
+}
+
+struct Chunked : IoReader {  // an io.Reader returning at most `step` bytes per call
+    Bytes b;
+    size_t at = 0, step = 1;
+    std::pair<size_t, Err> Read(uint8_t *p, size_t n) override {
+        if (at >= b.size()) return {0, Err::EOF_};
+        size_t k = std::min({n, step, b.size() - at});
+        std::memcpy(p, b.data() + at, k);
+        at += k;
+        return {k, Err::OK};
+    }
+};
+
+// --dump FILE: for every hex-encoded stream in FILE (one per line) its Dump, then what
+// Dumper::ReadFrom prints from reads of 7 bytes and the error it ends with, each followed by a
+// line "----": tests/test_cpp.py compares them with eazy_amd/dump.py (host only)
+static int dump_file(const char *path) {
+    FILE *f = std::fopen(path, "r");
+    if (!f) return 2;
+    std::string line;
+    int c;
+    for (;;) {
+        line.clear();
+        while ((c = std::fgetc(f)) != EOF && c != '\n') line += (char)c;
+        if (!line.empty()) {
+            std::printf("%s\n----\n", Dump(H(line)).c_str());
+            Buffer text;
+            auto d = NewDumper(&text);
+            Chunked r;
+            r.b = H(line);
+            r.step = 7;
+            auto [tot, err] = d->ReadFrom(&r);
+            std::printf("%s|%lld|%s\n----\n", std::string(text.b.begin(), text.b.end()).c_str(), (long long)tot, ez_strerror((int)err));
+        }
+        if (c == EOF) break;
+    }
+    std::fclose(f);
+    return 0;
+}
+
+// Dumper::ReadFrom with the stream in one read prints what one Write prints, and a stream cut
+// inside a token ends in UnexpectedEOF (reader.go:563-600).  (Reads that cut a token do not
+// print what Dump prints: like the reference, Write reports the bytes up to the cut token's
+// tag as taken; the comparison with the Python mirror covers that case.)
+static void TestDumperReadFrom() {
+    Bytes s = H("8003");  // (a meta header is not needed: the Dumper prints what it is given)
+    Encoder e;
+    s.clear();
+    e.MetaTag(s, MetaMagic, 4);
+    s = cat(s, B("eazy"));
+    e.MetaTag(s, MetaReset, 1);
+    s.push_back(20);
+    e.Tag(s, Literal, 5);
+    s = cat(s, B("hello"));
+    e.Tag(s, Copy, 10);
+    e.Offset(s, 5, 10);
+    s.push_back(0);
+    s.push_back(0);
+    e.Tag(s, Literal, 130);
+    for (int k = 0; k < 130; k++) s.push_back((uint8_t)(k * 7));
+    Dumper whole;
+    whole.GlobalOffset = -1;
+    CHECK(whole.Write(s).second == Err::OK);
+    for (size_t step : {s.size(), (size_t)4096}) {
+        Buffer text;
+        auto d = NewDumper(&text);
+        d->GlobalOffset = -1;
+        Chunked r;
+        r.b = s;
+        r.step = step;
+        auto [tot, err] = d->ReadFrom(&r);
+        CHECK(err == Err::OK && tot == (int64_t)s.size());
+        CHECK(std::string(text.b.begin(), text.b.end()) == whole.Text());
+    }
+    Chunked cut;
+    cut.b = sub(s, 0, s.size() - 3);
+    cut.step = cut.b.size();
+    Buffer sink;
+    auto d = NewDumper(&sink);
+    CHECK(d->ReadFrom(&cut).second == Err::UnexpectedEOF);
+    CHECK(Dump(sub(s, 0, s.size() - 3)).find("\nerror: short buffer") != std::string::npos);
+}
+
 int main(int argc, char **argv) {
+    if (argc > 2 && std::string(argv[1]) == "--dump") return dump_file(argv[2]);
     const bool cpu = argc > 1 && std::string(argv[1]) == "--cpu";
     run("TestPrintLengthEncoding", TestPrintLengthEncoding);
     run("TestPrintOffsetEncoding", TestPrintOffsetEncoding);
@@ -482,6 +602,7 @@ int main(int argc, char **argv) {
     run("TestEncoderPanics", TestEncoderPanics);
     run("TestErrorText", TestErrorText);
     run("TestCompressBound", TestCompressBound);
+    run("TestDumperReadFrom", TestDumperReadFrom);
     if (!cpu) {
         if (ez_device_count() <= 0) {
             std::printf("FAIL no MI355X visible\n");
@@ -503,6 +624,7 @@ int main(int argc, char **argv) {
         run("TestSinkFailureResets", TestSinkFailureResets);
         run("TestBatchMatchesWriter", TestBatchMatchesWriter);
         run("TestWriteBatch", TestWriteBatch);
+        run("TestHandleLeak", TestHandleLeak);
     }
     std::printf("%d/%d passed\n", g_run - g_fail, g_run);
     return g_fail ? 1 : 0;

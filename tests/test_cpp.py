@@ -24,10 +24,53 @@ def _run(*args):
 
 def test_cpp_host_only():
     out = _run("--cpu")
-    assert "6/6 passed" in out
+    assert "7/7 passed" in out
+
+
+def test_cpp_dump_matches_python_dumper(tmp_path):
+    """eazy::Dump (C++ mirror) prints what eazy_amd/dump.py prints, on the reference's KAT
+    streams, both fuzz corpora and the synthetic streams of the golden file (host only)."""
+    from golden_data import load
+
+    from eazy_amd import dump
+
+    g = load()
+    streams = [bytes.fromhex(e["input"]) for e in g["fuzz_reader"]]
+    for key in ("fuzz_writer", "synthetic_logs"):
+        for e in g[key]:
+            streams += [bytes.fromhex(v) for k, v in e.items() if k.startswith("stream_") and isinstance(v, str)]
+    # cut streams end in an error line
+    streams += [s[: len(s) // 2] for s in streams[-8:]]
+    assert len(streams) > 20
+    f = tmp_path / "streams.hex"
+    f.write_text("\n".join(s.hex() for s in streams) + "\n")
+    got = _run("--dump", str(f)).split("\n----\n")
+    assert len(got) >= 2 * len(streams)
+
+    class Chunks:  # reads of at most 7 bytes
+        def __init__(self, b):
+            self.b, self.at = b, 0
+
+        def read(self, k):
+            r = self.b[self.at : self.at + min(k, 7)]
+            self.at += len(r)
+            return r
+
+    from eazy_amd import _strerror
+
+    for k, s in enumerate(streams):
+        assert got[2 * k] == dump.Dump(s), s.hex()[:80]
+        sink = bytearray()
+
+        class W:
+            def write(self, b):
+                sink.extend(b)
+
+        tot, err = dump.NewDumper(W()).ReadFrom(Chunks(s))
+        assert got[2 * k + 1] == f"{sink.decode()}|{tot}|{_strerror(err)}", s.hex()[:80]
 
 
 @pytest.mark.gpu
 def test_cpp_full(cuda):
     out = _run()
-    assert "FAIL" not in out and "22/22 passed" in out
+    assert "FAIL" not in out and "24/24 passed" in out

@@ -344,7 +344,7 @@ def test_k2t_copy_chains_within_rounds(cuda):
     d_coff, d_offs = torch.from_numpy(coff).to(cuda), torch.from_numpy(offs).to(cuda)
     _, sz0, st0 = ez.decompress_batch(comp, d_coff, d_offs, exact_only=True)
     assert st0.abs().sum().item() == 0
-    for kind in ("t", "w", "r", ""):
+    for kind in ("t", "w", "r", "s", ""):
         ez.select_decompress_kernel(kind)
         try:
             out, sz, st = ez.decompress_batch(comp, d_coff, d_offs, max_len=max(lens))
@@ -354,3 +354,35 @@ def test_k2t_copy_chains_within_rounds(cuda):
         got = out[: int(offs[-1])].cpu().numpy().tobytes()
         for s, b in enumerate(bufs):
             assert got[offs[s] : offs[s + 1]] == b, f"K2 {kind!r}: stream {s} (len {lens[s]}) differs"
+
+
+@pytest.mark.gpu
+def test_decoder_routing_without_hint(cuda):
+    """The batch decoder follows the largest output slot, measured on the device when the
+    caller gives no max_len: C4-class buckets (4 MiB) take K2t, 16 KiB streams K2r, 4 KiB
+    streams K2s, each byte-exact against the input, with and without the hint."""
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    cases = [
+        ([b.tobytes() for b in np.split(synth.f32(5, 4 * (1 << 20)).view(np.uint8), 4)], "t"),
+        ([synth.logs(6 + k, 16 << 10).tobytes() for k in range(8)], "r"),
+        ([synth.logs(20 + k, 4096).tobytes() for k in range(40)] + [b"", b"x" * 17], "s"),
+    ]
+    for bufs, kind in cases:
+        want = [orc.compress(MiB, 1024, [b]) for b in bufs]
+        lens = [len(b) for b in bufs]
+        coff = np.concatenate([[0], np.cumsum([len(w) for w in want])]).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        comp = torch.from_numpy(np.frombuffer(b"".join(want) + bytes(64), np.uint8).copy()).to(cuda)
+        d_coff, d_offs = torch.from_numpy(coff).to(cuda), torch.from_numpy(offs).to(cuda)
+        for kw in ({}, {"max_len": max(lens)}):
+            out, sz, st = ez.decompress_batch(comp, d_coff, d_offs, **kw)
+            torch.cuda.synchronize()
+            assert ez.decompress_kernel_last() == kind, (kind, kw, ez.decompress_kernel_last())
+            assert st.abs().sum().item() == 0 and sz.cpu().tolist() == lens, kind
+            got = out[: int(offs[-1])].cpu().numpy().tobytes()
+            for s, b in enumerate(bufs):
+                assert got[offs[s] : offs[s + 1]] == b, f"{kind}: stream {s} differs"

@@ -122,7 +122,7 @@ def test_batch_decoder_errors_match_oracle(cuda):
     # the ring decoder with a small-slot hint on the same corpus
     cap = 8192
     ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-    for kind in ("r", "w", "t"):
+    for kind in ("s", "r", "w", "t"):
         ez.select_decompress_kernel(kind)
         try:
             out, sizes, status = ez.decompress_batch(comp, coff, ooff, max_len=cap)
@@ -171,7 +171,7 @@ def test_batch_decoders_on_damaged_streams(cuda):
     coff = torch.from_numpy(offs).to(cuda)
     for cap in (4096, 8192):
         ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-        for kind, kw in (("", {"max_len": cap}), ("r", {"max_len": cap}), ("w", {"max_len": cap}), ("t", {"max_len": cap}), ("", {}),
+        for kind, kw in (("", {"max_len": cap}), ("s", {"max_len": cap}), ("r", {"max_len": cap}), ("w", {"max_len": cap}), ("t", {"max_len": cap}), ("", {}),
                          ("", {"exact_only": True})):
             ez.select_decompress_kernel(kind)
             try:
@@ -228,7 +228,7 @@ def test_batch_decoders_ring_edge_distances(cuda):
     coff = torch.from_numpy(offs).to(cuda)
     cap = 72 << 10
     ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-    for kind in ("", "w", "r", "t"):
+    for kind in ("", "s", "w", "r", "t"):
         ez.select_decompress_kernel(kind)
         try:
             out, sizes, status = ez.decompress_batch(comp, coff, ooff, max_len=cap)

@@ -67,26 +67,22 @@ def test_oracle_uint32_position_wrap():
 def test_oracle_batch_spreads_few_streams_over_threads():
     """The CPU baseline's batch runner: a batch of only 64 long streams must
     use every thread (work grains of count / (threads * 4) streams, not 64),
-    and give the same bytes as one thread."""
+    and give the same bytes as one thread.  (The grain is asserted, not a
+    wall-clock speedup: timings on a shared host are noise.)"""
     import os
-    import time
 
     import numpy as np
 
     from eazy_amd import synth
 
+    assert orc.batch_grain(64, 16) == 1 and orc.batch_grain(64, 8) == 2
+    assert orc.batch_grain(65536, 16) == 64 and orc.batch_grain(10, 1) == 2 and orc.batch_grain(0, 4) == 1
     threads = min(8, os.cpu_count() or 1)
-    if threads < 4:
-        pytest.skip("needs >= 4 host CPUs")
     count, size = 64, 64 << 10
+    # every thread gets at least 4 tasks
+    assert count // orc.batch_grain(count, threads) >= 4 * threads
     data = synth.logs(13, count * size)
     offs = (np.arange(count + 1) * size).astype(np.int64)
     slot = (np.arange(count + 1) * (size + size // 4 + 32)).astype(np.int64)
-    t = {}
-    res = {}
-    for n in (1, threads):
-        t0 = time.perf_counter()
-        res[n] = orc.compress_batch(1 << 20, 1024, data, offs, slot, n)
-        t[n] = time.perf_counter() - t0
+    res = {n: orc.compress_batch(1 << 20, 1024, data, offs, slot, n) for n in (1, threads)}
     assert np.array_equal(res[1][1], res[threads][1]) and np.array_equal(res[1][0], res[threads][0])
-    assert t[1] / t[threads] > 2, f"{threads} threads only {t[1] / t[threads]:.2f}x faster than one"
