@@ -138,19 +138,20 @@ def source_hash() -> str:
 
 
 def load_traffic(path, workload, count, size, dom):
-    """HBM bytes per launch of the dominant stage from a PMC summary
-    (FETCH_SIZE x 2 + WRITE_SIZE summed over the stage's kernels; gfx950
-    correction in tools/traffic.py) -> (bytes or None, provenance)."""
+    """HBM bytes per launch of the dominant stage from a PMC summary (FETCH_SIZE +
+    WRITE_SIZE summed over the stage's kernels, FETCH_SIZE doubled only for the
+    coalesced-stream kernels, tools/traffic.py) -> (bytes or None, provenance,
+    {"raw": FETCH_SIZE as counted, "x2": every FETCH_SIZE doubled} or None)."""
     if path is None:
         path = os.path.join(ROOT, "profiles", f"traffic_{workload}.json")
         if not os.path.exists(path):
-            return None, "no committed PMC summary for this workload"
+            return None, "no committed PMC summary for this workload", None
         t = json.load(open(path))
         key = (t.get("source_hash"), t.get("streams"), t.get("stream_bytes"))
         if key != (source_hash(), count, size):
-            return None, f"{os.path.relpath(path, ROOT)} was measured on other kernel sources or shape"
+            return None, f"{os.path.relpath(path, ROOT)} was measured on other kernel sources or shape", None
     elif not os.path.exists(path):
-        return None, f"{path} missing"
+        return None, f"{path} missing", None
     else:
         t = json.load(open(path))
     kern = t.get("kernels", t)
@@ -159,10 +160,13 @@ def load_traffic(path, workload, count, size, dom):
     # times counts every dispatch)
     pre = {"k1_compress": ("k1_", "kx_"), "k2_decompress": ("k2_", "kd_"), "k3_pack": ("k3_",)}[dom]
     # (per_step is null in a profile without a k3_gather dispatch to count steps by: the per-launch figure)
-    vals = [v["per_step"] if v.get("per_step") is not None else v["traffic"] for k, v in kern.items()
-            if k.startswith(pre) and v.get("traffic")]
+    def stage(key, per):
+        vals = [v[per] if v.get(per) is not None else v.get(key) for k, v in kern.items() if k.startswith(pre) and v.get(key)]
+        return sum(vals) if vals else None
+
     src = os.path.relpath(path, ROOT) if path.startswith(ROOT) else path
-    return (sum(vals) if vals else None), f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, {src}"
+    alt = {"raw": stage("traffic_raw", "per_step_raw"), "x2": stage("traffic_x2", "per_step_x2")}
+    return stage("traffic", "per_step"), f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes, {src}", alt
 
 
 def _oracle_pass(orc, host, offs, block, htable, threads, seconds, g_packed=None, g_off=None):
@@ -610,7 +614,7 @@ def main():
     dom = max(kern, key=kern.get)
     alg = total + comp_bytes  # per launch on this rank (n + c), SURVEY.md §8d
     achieved = alg / (kern[dom] / 1e3) / 1e9
-    traffic, traffic_src = load_traffic(args.traffic_json, wl, count, size, dom)
+    traffic, traffic_src, traffic_alt = load_traffic(args.traffic_json, wl, count, size, dom)
 
     par = (f"dp{world}: one global batch in contiguous whole-stream shards; RCCL all-gather of per-stream sizes "
            f"-> global offsets in the step" if sharded else
@@ -649,6 +653,11 @@ def main():
             "unit": "GB/s",
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
+            "traffic_raw": (traffic_alt or {}).get("raw"),
+            "traffic_all_fetch_doubled": (traffic_alt or {}).get("x2"),
+            "traffic_note": "HBM-side bytes per step of the dominant stage (FETCH_SIZE + WRITE_SIZE); FETCH_SIZE "
+                            "doubled (the guide's gfx950 correction) only for coalesced-stream kernels, raw for the "
+                            "scattered-gather kernels; Infinity-Cache hits are counted",
             "traffic_source": traffic_src,
             "source_hash": source_hash(),
             "algorithmic_bytes_per_launch": alg,

@@ -31,6 +31,10 @@
 #include "ez_bytes.h"
 #include "ez_k2_parse.h"
 
+#ifndef EZ_EXP
+#define EZ_EXP 0  // timing builds only: 2^21 no copies, 2^22 no literals, 2^23 no rounds, 2^24 no store
+#endif
+
 namespace ez {
 
 namespace {
@@ -54,11 +58,19 @@ __device__ __forceinline__ V16 ld_batch(const uint8_t *y, const uint8_t *lo, con
 // ---------------------------------------------------------------------------------------------
 // K2p: the token walk, a lane per stream
 // ---------------------------------------------------------------------------------------------
+// The walk's chain is one LDS byte read per token: a table holds, for every input position of the
+// lane's window, the input bytes a token starting there takes (SWAR over 4 positions a word, the
+// common forms only: a 1-byte tag with a plain, Off1 or Off2 offset for a copy; 0 for the rest,
+// which the walk parses in full) with bit 7 set when the position holds a tag (not padding).  The
+// table is built when a refill lands, so the walk itself is a byte read, a mark and an add.
+// Everything that needs the output position (slot room, the window, BlockSizeLimit) is checked
+// by K2q, which parses every token anyway.
 constexpr int kPBlock = 256;
 constexpr int32_t kPRing = 256;                // input ring bytes per lane
 constexpr int32_t kPStride = kPRing + 16;      // + a mirror of its first 16 bytes
+constexpr int32_t kPTab = kPBlock * kPStride;  // the step tables after the rings (kPRing bytes per lane)
 constexpr int32_t kPRefill = 128;              // bytes a lane's refill brings
-constexpr int kPStep = 8;                      // tokens parsed per refill step (<= 16 bytes each)
+constexpr int kPStep = 8;                      // tokens walked per refill step (<= 16 bytes each)
 
 // the refill of one lane: 128 bytes of the stream from input position at
 struct Refill {
@@ -77,7 +89,34 @@ __device__ __forceinline__ void refill_issue(Refill &r, const uint8_t *y, const 
     }
 }
 
-__device__ __forceinline__ void refill_commit(const Refill &r, uint8_t *ring, int32_t at) {
+__device__ __forceinline__ uint32_t fanout(uint32_t f) { return f | (f - (f >> 7)); }  // bit 7 of a byte -> 0xff
+
+// Step-table bytes of 4 positions: X = bytes x .. x+3, Y = bytes x+1 .. x+4.  The input bytes a
+// token starting there takes for the common forms (reader.go:346-392, 422-472): a literal with a
+// 1-byte tag (length < 124; a zero byte is padding, one byte), a copy with a 1-byte tag and a
+// plain, Off1 or Off2 offset; 0 for the others (Len1/Len2/Len4 tags, metas, Off4 and OffLong
+// offsets).  Bit 7: the byte is a tag (not padding).
+__device__ __forceinline__ uint32_t swar_step(uint32_t X, uint32_t Y) {
+    const uint32_t X7 = X & 0x7f7f7f7fu, Y7 = Y & 0x7f7f7f7fu;
+    const uint32_t isc = X & 0x80808080u;                         // a copy's (or a meta's) tag
+    const uint32_t lit = X7 + 0x01010101u;                         // 1 + length
+    const uint32_t ge252 = (Y7 + 0x04040404u) & Y & 0x80808080u;  // offset byte >= 252
+    const uint32_t ge254 = (Y7 + 0x02020202u) & Y & 0x80808080u;  // >= 254: Off4, OffLong
+    const uint32_t cpy = 0x02020202u + (((Y & 0x03030303u) + 0x01010101u) & fanout(ge252));
+    const uint32_t mc = fanout(isc);
+    const uint32_t adv = (cpy & mc) | (lit & ~mc);
+    const uint32_t lwide = (X7 + 0x04040404u) & 0x80808080u;      // length byte >= 124
+    const uint32_t nz = (X7 + 0x7f7f7f7fu) & 0x80808080u;         // low 7 bits nonzero (else 0x80: meta)
+    const uint32_t rare = lwide | (isc & ~nz) | (isc & ge254);
+    const uint32_t tag = (nz | isc) & ~rare;                       // a token's tag: bit 7 of its byte
+    return (adv & ~fanout(rare)) | tag;
+}
+
+// a refill landed: its 128 bytes into the ring, and the step table of positions at - 8 .. at + 119
+// (the 8 bytes before it are in the ring already; positions at + 120 .. at + 127 need bytes of the
+// next refill and are written with it)
+__device__ __forceinline__ void refill_commit(const Refill &r, uint8_t *ring, uint8_t *tab, int32_t at) {
+    const uint64_t before = *(const u64_ua *)(ring + ((at - 8) & (kPRing - 1)));  // (garbage at a restart: never read)
 #pragma unroll
     for (int k = 0; k < kPRefill / 16; k++) {
         const int32_t slot = (at + 16 * k) & (kPRing - 1);
@@ -88,12 +127,37 @@ __device__ __forceinline__ void refill_commit(const Refill &r, uint8_t *ring, in
             *(u64_ua *)(ring + kPRing + 8) = r.v[k].hi;
         }
     }
+    // dwords d[0..33]: bytes at - 8 .. at + 127
+    uint32_t d[34];
+    d[0] = (uint32_t)before;
+    d[1] = (uint32_t)(before >> 32);
+#pragma unroll
+    for (int k = 0; k < kPRefill / 16; k++) {
+        d[2 + 4 * k] = (uint32_t)r.v[k].lo;
+        d[3 + 4 * k] = (uint32_t)(r.v[k].lo >> 32);
+        d[4 + 4 * k] = (uint32_t)r.v[k].hi;
+        d[5 + 4 * k] = (uint32_t)(r.v[k].hi >> 32);
+    }
+#pragma unroll
+    for (int k = 0; k < kPRefill / 16; k++) {  // 16 positions (4 words) per store
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int x = 4 * k + q;
+            w[q] = swar_step(d[x], __builtin_amdgcn_alignbyte(d[x + 1], d[x], 1));
+        }
+        const int32_t slot = (at - 8 + 16 * k) & (kPRing - 1);
+        *(u64_ua *)(tab + slot) = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        *(u64_ua *)(tab + slot + 8) = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+    }
 }
 
 // the token walk of stream s (valid: s < count) with `ring` (kPStride bytes of LDS) as its input
-// window; writes its region of the bitmap workspace (kSmallRegion words: [0] the token count or
-// kSHandOver, then one bit per input byte set at every literal or copy token's first byte)
-__device__ __forceinline__ void pre_one(const DecompressArgs &A, const uint64_t s, const bool valid, uint8_t *ring, uint32_t *bm) {
+// window and `tab` (kPRing bytes) as its step table; writes its region of the bitmap workspace
+// (kSmallRegion words: [0] the token count | log2 of the window << 16, or kSHandOver; then one bit
+// per input byte, set at every literal or copy token's first byte)
+__device__ __forceinline__ void pre_one(const DecompressArgs &A, const uint64_t s, const bool valid, uint8_t *ring, uint8_t *tab,
+                                        uint32_t *bm) {
     const uint64_t sc = valid ? s : 0;
     const uint8_t *b = A.in + A.in_off[sc];
     const int64_t nb64 = (int64_t)(A.in_off[sc + 1] - A.in_off[sc]);
@@ -105,8 +169,8 @@ __device__ __forceinline__ void pre_one(const DecompressArgs &A, const uint64_t 
     // what K2s takes: slots of <= 4 KiB, streams of <= kSmallIn bytes, batches of >= 16 bytes
     const bool fits = in_end - A.in >= 16 && nb64 <= kSmallIn && cap64 <= kSmallOut;
     bool live = valid && fits, ho = valid && !fits;
-    const int32_t nb = live ? (int32_t)nb64 : 0, cap = (int32_t)cap64;
-    int32_t i = 0, pos = 0, bsl = -1, win = 0, ntok = 0;
+    const int32_t nb = live ? (int32_t)nb64 : 0;
+    int32_t i = 0, bsl = -1, ntok = 0;
     int32_t F = 0;       // the ring holds input [F - kPRing, F) (what has been committed)
     int32_t cw = 0;      // bitmap word being built
     uint32_t acc = 0;
@@ -115,7 +179,7 @@ __device__ __forceinline__ void pre_one(const DecompressArgs &A, const uint64_t 
     // prologue: the first 128 bytes, waited for
     if (any_lane(live)) {
         refill_issue(r, b, A.in, in_end);
-        if (live) refill_commit(r, ring, 0);
+        if (live) refill_commit(r, ring, tab, 0);
         F = live ? kPRefill : 0;
     }
     while (any_lane(live)) {
@@ -126,32 +190,28 @@ __device__ __forceinline__ void pre_one(const DecompressArgs &A, const uint64_t 
         if (any_lane(rf)) {
             if (rf) refill_issue(r, b + F, A.in, in_end);
         }
-        // up to kPStep tokens from the ring while the refill is in flight
+        // up to kPStep tokens while the refill is in flight
 #pragma unroll 1
         for (int st = 0; st < kPStep; st++) {
             const bool rd = live && i + 16 <= F;
             if (!any_lane(rd)) break;
-            const V16 h = lds16(ring + (i & (kPRing - 1)));
-            int32_t L, adv;
-            uint32_t D;
-            bool cp;
-            const int32_t ft = fast_tok(h.lo, L, adv, D, cp);
-            const bool f = (ft | bsl | (nb - i - adv) | (cap - pos - L) | (lim32 - L) | (cp ? win - (int32_t)D : 0)) >= 0;
-            bool tok = true, bad = false;
-            if (any_lane(rd && !f)) {
-                if (rd && !f) {
+            const uint32_t e = tab[i & (kPRing - 1)];
+            int32_t adv = (int32_t)(e & 0x7f);
+            bool tok = (e & 0x80) != 0, bad = false;
+            if (any_lane(rd && adv == 0)) {  // a rare form: the full parse of its 16 bytes
+                if (rd && adv == 0) {
                     K2Tok t;
-                    const int rr = k2_parse(h, i, nb, pos, cap, lim32, limit, bsl, t);
-                    if (rr == kParseHandOver) {
-                        bad = true;
-                    } else {
-                        L = t.L;
-                        adv = t.adv;
-                        tok = rr == kParseToken;
-                        win = bsl < 0 ? 0 : (bsl >= 30 ? 0x7fffffff : 1 << bsl);
+                    const int rr = k2_scan(lds16(ring + (i & (kPRing - 1))), i, nb, lim32, limit, t);
+                    adv = t.adv;
+                    tok = rr == kParseToken;
+                    if (rr == kScanReset) {
+                        if (ntok != 0) bad = true;  // MetaReset only before any output (k2_check)
+                        bsl = (int32_t)t.marg;
                     }
+                    bad = bad || rr == kParseHandOver;
                 }
             }
+            bad = bad || (tok && bsl < 0);  // a token before the window is set
             const bool go = rd && !bad;
             const bool mark = go && tok;
             // the bitmap: a word is stored when the walk leaves it (the words it jumps over are 0)
@@ -168,21 +228,21 @@ __device__ __forceinline__ void pre_one(const DecompressArgs &A, const uint64_t 
             }
             acc = mark ? acc | (1u << (i & 31)) : acc;
             ntok += mark ? 1 : 0;
-            pos = go ? pos + (tok ? L : 0) : pos;
             i = go ? i + adv : i;
             ho = ho || (rd && bad);
             live = live && !(rd && bad) && i < nb;
         }
         if (any_lane(rf)) {
-            if (rf) refill_commit(r, ring, F);
+            if (rf) refill_commit(r, ring, tab, F);
         }
         F = rf ? F + kPRefill : F;
     }
-    if (valid && !ho) {  // the last word, the words after it, the count
+    ho = ho || (valid && fits && i > nb);  // the last token runs past the input
+    if (valid && !ho) {  // the last word, the words after it, the count and the window
         const int32_t nw = (nb + 31) >> 5;
         if (nw > 0) reg[1 + cw] = acc;
         for (int32_t x = cw + 1; x < nw; x++) reg[1 + x] = 0;
-        reg[0] = (uint32_t)ntok;
+        reg[0] = (uint32_t)ntok | ((uint32_t)(bsl < 0 ? 0 : bsl) << 16);
     }
     if (ho) {
         reg[0] = kSHandOver;
@@ -193,10 +253,10 @@ __device__ __forceinline__ void pre_one(const DecompressArgs &A, const uint64_t 
 
 __global__ __launch_bounds__(kPBlock) void k2_pre(DecompressArgs A, uint32_t *bm) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    uint8_t *ring = smem + threadIdx.x * kPStride;
+    uint8_t *ring = smem + threadIdx.x * kPStride, *tab = smem + kPTab + threadIdx.x * kPRing;
     for (uint64_t s0 = (uint64_t)blockIdx.x * kPBlock; s0 < A.count; s0 += (uint64_t)gridDim.x * kPBlock) {
         const uint64_t s = s0 + threadIdx.x;
-        pre_one(A, s, s < A.count, ring, bm);
+        pre_one(A, s, s < A.count, ring, tab, bm);
     }
 }
 
@@ -275,17 +335,47 @@ __device__ __forceinline__ V16 out16(const uint8_t *ob, int32_t x) {
 
 __device__ __forceinline__ int32_t run_step_of(int32_t per) { return per * (16 / per); }
 
-// streams s .. s+3 of a wave (s = base + row); ob: the row's LDS output, list, trash
+// the 64 input bytes at y (clamped into the batch near its end: bytes past it read 0)
+struct In64 {
+    V16 v[4];
+};
+__device__ __forceinline__ In64 ld64(const uint8_t *y, const uint8_t *lo, const uint8_t *hi) {
+    In64 r;
+    if (any_lane(y + 64 > hi)) {
+#pragma unroll
+        for (int q = 0; q < 4; q++) r.v[q] = ld_batch(y + 16 * q, lo, hi);
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; q++) r.v[q] = ld16v(y + 16 * q);
+    }
+    return r;
+}
+// bytes j + o .. j + o + 15 of the 64 (o = 0, 16, 32, 48; bytes past the 64 read 0), j <= 16
+__device__ __forceinline__ V16 at64(const In64 &a, uint32_t j, int o) {
+    const V16 x = a.v[o / 16];
+    const V16 y = o / 16 + 1 < 4 ? a.v[o / 16 + 1] : V16{0, 0};
+    return at32(x, y, j);
+}
+
+// the streams base .. base+3 of a wave, one per row (s = base + row); ob: the row's LDS output
+// (16 zero bytes before it), list: its token list, trash: 8 bytes of this lane's
 __device__ __forceinline__ void small_one(const DecompressArgs &A, const uint32_t *bm, const uint64_t s, const int k, uint8_t *ob,
                                           uint16_t *list, uint8_t *trash) {
     const bool v0 = s < A.count;
     const uint64_t sc = v0 ? s : 0;
     const uint32_t *reg = bm + sc * (uint64_t)kSmallRegion;
-    const bool valid = v0 && reg[0] != kSHandOver;
+    const uint32_t w0r = reg[0];
+    bool valid = v0 && w0r != kSHandOver;
     const uint8_t *b = A.in + A.in_off[sc];
     const uint8_t *in_end = A.in + A.in_off[A.count];
     const int32_t nb = valid ? (int32_t)(A.in_off[sc + 1] - A.in_off[sc]) : 0;
+    const int32_t cap = valid ? (int32_t)(A.out_off[sc + 1] - A.out_off[sc]) : 0;  // (<= kSmallOut: K2p)
+    const int64_t limit = A.block_size_limit;
+    const int32_t lim32 = limit == 0 || limit > 0x7fffffff ? 0x7fffffff : (int32_t)limit;
+    const uint32_t bsl = (w0r >> 16) & 63;
+    const int32_t win = bsl >= 30 ? 0x7fffffff : 1 << bsl;
     const int32_t nwd = (nb + 31) >> 5;  // bitmap words
+    const uint32_t rsh = (uint32_t)(threadIdx.x & 48);
     int32_t pos = 0;
     uint32_t wnext = k < nwd ? reg[1 + k] : 0;
 #pragma unroll 1
@@ -295,7 +385,7 @@ __device__ __forceinline__ void small_one(const DecompressArgs &A, const uint32_
         wnext = w0 + kQG + k < nwd ? reg[1 + w0 + kQG + k] : 0;  // (the next chunk's words, in flight)
         const int32_t c = __builtin_popcount(word);
         const int32_t ci = row_incl_sum(c);
-        const int32_t nt = row_last(ci);
+        const int32_t nt = valid ? row_last(ci) : 0;
         int32_t e = ci - c;
         const int32_t wbase = (w0 + k) << 5;
         while (any_lane(word != 0)) {
@@ -304,32 +394,23 @@ __device__ __forceinline__ void small_one(const DecompressArgs &A, const uint32_
                 word &= word - 1;
             }
         }
-        // ---- rounds of 16 tokens, one per lane; the next round's headers load during this one
-        V16 n0{0, 0}, n1{0, 0};
-        {
-            const int32_t q = k < nt ? (int32_t)list[k] : 0;
-            n0 = ld_batch(b + q, A.in, in_end);
-            n1 = ld_batch(b + q + 16, A.in, in_end);
-        }
+        // ---- rounds of 16 tokens, one per lane; the next round's 64 bytes load during this one
+        In64 nx = ld64(b + (k < nt ? (int32_t)list[k] : 0), A.in, in_end);
 #pragma unroll 1
-        for (int32_t t0 = 0; any_lane(t0 < nt); t0 += kQG) {
-            const bool has = t0 + k < nt;
+        for (int32_t t0 = 0; !(EZ_EXP & (1 << 23)) && any_lane(t0 < nt); t0 += kQG) {
+            const bool has = valid && t0 + k < nt;
             const int32_t q = has ? (int32_t)list[t0 + k] : 0;
-            const V16 a0 = n0, a1 = n1;
-            {
-                const int32_t qn = t0 + kQG + k < nt ? (int32_t)list[t0 + kQG + k] : 0;
-                n0 = ld_batch(b + qn, A.in, in_end);
-                n1 = ld_batch(b + qn + 16, A.in, in_end);
-            }
-            // ---- the token (K2p checked every one: the common forms branch-free, the long ones by k2_scan)
+            const In64 a = nx;
+            nx = ld64(b + (t0 + kQG + k < nt ? (int32_t)list[t0 + kQG + k] : 0), A.in, in_end);
+            // ---- the token (K2p found it: the common forms branch-free, the long ones by k2_scan)
             int32_t L, fadv, j = 1;
             uint32_t Du;
             bool cp;
-            const int32_t ft = fast_tok(a0.lo, L, fadv, Du, cp);
+            const int32_t ft = fast_tok(a.v[0].lo, L, fadv, Du, cp);
             if (any_lane(has && ft < 0)) {
                 if (has && ft < 0) {
                     K2Tok t;
-                    (void)k2_scan(a0, q, nb, 0x7fffffff, 0, t);
+                    (void)k2_scan(a.v[0], q, nb, 0x7fffffff, 0, t);
                     L = t.L;
                     j = t.j;
                     Du = t.D;
@@ -342,18 +423,34 @@ __device__ __forceinline__ void small_one(const DecompressArgs &A, const uint32_
             const int32_t incl = row_incl_sum(L);
             const int32_t total = row_last(incl);
             const int32_t dst = pos + incl - L;
-            // ---- literals: their bytes from the 32 loaded at the token's start, or the input
-            const bool lit = has && !cp;
-            put_exact(lit ? ob + dst : trash, at32(a0, a1, (uint32_t)j), lit ? (uint32_t)(L < 16 ? L : 16) : 0u, trash);
-#pragma unroll 1
-            for (int32_t p = 16; any_lane(lit && p < L); p += 16) {
-                const bool act = lit && p < L;
-                V16 v = shr16(a1, (uint32_t)j);  // bytes j+16 .. 31: enough when L <= 32 - j
-                const bool ld = act && (p > 16 || L > 32 - j);
-                if (any_lane(ld)) {
-                    if (ld) v = ld_batch(b + q + j + p, A.in, in_end);
+            // the checks on the output position (k2_check, reader.go:251-263): room in the slot, the
+            // block size limit, the window; a stream failing one goes to the exact decoder whole
+            const bool bad = has && ((uint32_t)pos + (uint32_t)incl > (uint32_t)cap || L > lim32 || (cp && D > win));
+            if ((uint32_t)(__builtin_amdgcn_ballot_w64(bad) >> rsh) & 0xffffu) {
+                if (valid && k == 0) {
+                    const uint32_t at = atomicAdd(&A.slow[0], 1u);
+                    A.slow[1 + at] = (uint32_t)s;
                 }
-                put_exact(act ? ob + dst + p : trash, v, act ? (uint32_t)(L - p < 16 ? L - p : 16) : 0u, trash);
+                valid = false;
+            }
+            const bool live = valid && has;
+            // ---- literals: up to 64 - j bytes from the loaded ones, the rest from the input
+            const bool lit = live && !cp && !(EZ_EXP & (1 << 22));
+            put_exact(lit ? ob + dst : trash, at64(a, (uint32_t)j, 0), lit ? (uint32_t)(L < 16 ? L : 16) : 0u, trash);
+            if (any_lane(lit && L > 16)) {
+#pragma unroll
+                for (int o = 16; o < 64; o += 16) {
+                    const bool act = lit && L > o;
+                    if (any_lane(act)) put_exact(act ? ob + dst + o : trash, at64(a, (uint32_t)j, o), act ? (uint32_t)(L - o < 16 ? L - o : 16) : 0u, trash);
+                }
+#pragma unroll 1
+                for (int32_t o = 64 - j; any_lane(lit && o < L); o += 16) {  // (past the loaded bytes: rare)
+                    const bool act = lit && o < L;
+                    if (act) {
+                        const V16 v = ld_batch(b + q + j + o, A.in, in_end);
+                        put_exact(ob + dst + o, v, (uint32_t)(L - o < 16 ? L - o : 16), trash);
+                    }
+                }
             }
             // ---- copies in batches: a batch runs from the first pending copy up to the first one
             // whose source reaches past that copy's output position (the output before it is final);
@@ -361,8 +458,7 @@ __device__ __forceinline__ void small_one(const DecompressArgs &A, const uint32_
             const int32_t cs = dst - D;
             const int32_t need = cs + (D < L ? D : L);
             const bool fre = cp && (D == 0 || need <= pos);
-            bool pend = cp;
-            const uint32_t rsh = (uint32_t)(threadIdx.x & 48);
+            bool pend = live && cp && !(EZ_EXP & (1 << 21));
 #pragma unroll 1
             while (any_lane(pend)) {
                 const int32_t oa = row_min(pend ? dst : 0x7fffffff);
@@ -371,21 +467,32 @@ __device__ __forceinline__ void small_one(const DecompressArgs &A, const uint32_
                 const int32_t bnd = (int32_t)__builtin_ctz(bb | 0x10000u);
                 const bool ex = pend && (fre || k < bnd);
                 pend = pend && !ex;
-                // the common copy: D >= 16, at most 16 bytes: one read, one write
-                int32_t stp = 16;
-                V16 pv{0, 0};
+                // a copy that does not read its own output (D >= L, or a zero region): up to 64 bytes
+                // read before any is written; a self-overlapping one 16 bytes at a time (D >= 16), or
+                // a run of period D < 16 as its 16-byte pattern every run_step bytes
                 const bool run = ex && D > 0 && D < 16;
+                const bool wide = D >= L || D == 0;
+                int32_t stp = wide ? 64 : 16;
+                V16 pv{0, 0};
                 if (any_lane(run)) {
                     if (run) {
                         pv = run_pattern(shr16(out16(ob, dst - 16), (uint32_t)(16 - D)), (uint32_t)D);
                         stp = run_step_of(D);
                     }
                 }
+                const bool src = D >= 16;
                 int32_t o = 0;
                 while (any_lane(ex && o < L)) {
                     const bool act = ex && o < L;
-                    const V16 v = D >= 16 ? out16(ob, cs + o) : pv;  // (D == 0: zeros)
-                    put_exact(act ? ob + dst + o : trash, v, act ? (uint32_t)(L - o < 16 ? L - o : 16) : 0u, trash);
+                    V16 v[4];
+#pragma unroll
+                    for (int p = 0; p < 4; p++) v[p] = src ? out16(ob, cs + o + 16 * p) : pv;
+                    put_exact(act ? ob + dst + o : trash, v[0], act ? (uint32_t)(L - o < 16 ? L - o : 16) : 0u, trash);
+#pragma unroll
+                    for (int p = 1; p < 4; p++) {
+                        const bool ap = act && wide && L > o + 16 * p;
+                        if (any_lane(ap)) put_exact(ap ? ob + dst + o + 16 * p : trash, v[p], ap ? (uint32_t)(L - o - 16 * p < 16 ? L - o - 16 * p : 16) : 0u, trash);
+                    }
                     o += stp;
                 }
             }
@@ -393,7 +500,7 @@ __device__ __forceinline__ void small_one(const DecompressArgs &A, const uint32_
         }
     }
     // ---- the output to its slot, 256 bytes per row and step
-    if (valid) {
+    if (valid && !(EZ_EXP & (1 << 24))) {
         uint8_t *out = A.out + A.out_off[sc];
         for (int32_t x = 16 * k; x < pos; x += 16 * kQG) {
             const V16 v = lds16(ob + x);
@@ -424,12 +531,12 @@ __global__ __launch_bounds__(kQBlock) void k2_small(DecompressArgs A, const uint
 hipError_t launch_decompress_small(const DecompressArgs &a, uint32_t *bm, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k2_pre, hipFuncAttributeMaxDynamicSharedMemorySize, kPBlock * kPStride);
+        (void)hipFuncSetAttribute((const void *)k2_pre, hipFuncAttributeMaxDynamicSharedMemorySize, kPTab + kPBlock * kPRing);
         (void)hipFuncSetAttribute((const void *)k2_small, hipFuncAttributeMaxDynamicSharedMemorySize, kQPer * kQStride);
         attr_done = true;
     }
     const uint64_t gp = (a.count + kPBlock - 1) / kPBlock;
-    hipLaunchKernelGGL(k2_pre, dim3((unsigned)(gp < (1u << 30) ? gp : (1u << 30))), dim3(kPBlock), kPBlock * kPStride, st, a, bm);
+    hipLaunchKernelGGL(k2_pre, dim3((unsigned)(gp < (1u << 30) ? gp : (1u << 30))), dim3(kPBlock), kPTab + kPBlock * kPRing, st, a, bm);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     const uint64_t gq = (a.count + kQPer - 1) / kQPer;

@@ -91,6 +91,24 @@ def test_bench_launches_ranks_itself():
     assert res["bytes_gathered"] == 67 * 300
 
 
+def test_c3_rehearsal_full_size():
+    """C3 at full size on the CPU: `bench.py --gpus 8 --rehearse` over 1,048,576 x 4 KiB
+    streams (gloo, 8 ranks: 131,072-stream shards, an 8 MiB int64 size all-gather, the
+    global offsets, the 4 GiB payload gather to rank 0, checked against the input)."""
+    import json
+
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    bench = os.path.join(os.path.dirname(HERE), "bench.py")
+    p = subprocess.run([sys.executable, bench, "--gpus", "8", "--rehearse", "--streams", "1048576", "--stream-bytes", "4096"],
+                       env=env, capture_output=True, text=True, timeout=900)
+    assert p.returncode == 0, p.stderr[-3000:]
+    res = json.loads([ln for ln in p.stdout.splitlines() if ln.startswith("{")][0])
+    assert res["n_gpus"] == 8 and res["streams_per_rank"] == [131072] * 8 and res["gathered_equals_input"]
+    assert res["bytes_gathered"] == 1048576 * 4096
+
+
 def test_bench_rejects_world_mismatch():
     """--gpus must equal the world size the launch ends up with."""
     env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
