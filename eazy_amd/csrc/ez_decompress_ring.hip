@@ -88,9 +88,23 @@ __host__ __device__ __forceinline__ void ring_st(uint8_t *ring, int32_t p, V16 v
     *(u64_ua *)(ring + r2 + 8) = v.hi;
 }
 
+// bytes o .. o+15 (0 <= o <= 16) of the 32 bytes (a, b)
+__host__ __device__ __forceinline__ V16 win16(V16 a, V16 b, uint32_t o) {
+    const uint32_t q = o >> 3, r = o & 7;
+    const uint64_t w0 = q == 0 ? a.lo : (q == 1 ? a.hi : b.lo);
+    const uint64_t w1 = q == 0 ? a.hi : (q == 1 ? b.lo : b.hi);
+    const uint64_t w2 = q == 0 ? b.lo : b.hi;  // (q == 2: o == 16, r == 0: w2 unused)
+    return V16{fun8(w0, w1, r), fun8(w1, w2, r)};
+}
+
 // decodes stream s with `ring` (kRing + 16 bytes, with 16-byte guards on both sides) as its history; false = hand
 // the stream over (host-compilable: tools/ring_emu.hip runs it on the CPU)
 // fper: iterations between flushes (a power of two <= kMaxFlushPer)
+// HW: the headers come from a 32-byte window of 16-byte-aligned input loads, reloaded only when the
+// next header leaves it (a token takes ~5 input bytes at C1: one aligned pair per ~3 tokens, each
+// 16-byte aligned load one access of the vector memory path), instead of one byte-unaligned 16-byte
+// load (one access per dword it touches) per token
+template <bool HW>
 __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring, uint32_t fper = 8) {
     const uint8_t *b = A.in + A.in_off[s];
     const int64_t nb64 = (int64_t)(A.in_off[s + 1] - A.in_off[s]);
@@ -109,8 +123,19 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     int32_t i = 0, pos = 0, bsl = -1;  // bsl: log2 of the window after MetaReset (-1: none yet)
     int32_t win = 0;                   // the window's size once bsl is set (copies farther hand over)
     V16 h{0, 0};                       // 16 bytes at b + i (the next header)
-    if (!slow) h = ld_in(b, A.in, in_end);
     int32_t hd = 0;  // a header loaded from the batch's last 16 bytes: its shift, applied after the wait
+    // HW: the input [wb, wb + 32) (wb 16-byte aligned) in hw0, hw1; the next header at wb + hd
+    const uint8_t *wb = (const uint8_t *)((uintptr_t)b & ~(uintptr_t)15);
+    V16 hw0{0, 0}, hw1{0, 0};
+    if (!slow) {
+        if (HW) {
+            hw0 = ld_clamped16(wb, A.in, in_end);
+            hw1 = ld_clamped16(wb + 16, A.in, in_end);
+            hd = (int32_t)(b - wb);
+        } else {
+            h = ld_in(b, A.in, in_end);
+        }
+    }
     // the token being written: rem bytes at dst from sp (input / HBM output) or from the ring
     int32_t rem = 0, dst = 0, step = 16, rp = 0, fl = 0;  // fl: output below it is in HBM
     uint32_t it = 0;
@@ -130,7 +155,9 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     // parse no longer waits behind the move's HBM read, nor the move behind the parse.
     // (every lane loads in every iteration; lanes are live only if the batch holds >= 16 bytes)
     for (bool go = any_lane(live); go; go = any_lane(live)) {
-        if (any_lane(hd != 0)) {
+        if (HW) {
+            h = win16(hw0, hw1, (uint32_t)hd);
+        } else if (any_lane(hd != 0)) {
             if (hd != 0) h = shr16(h, (uint32_t)hd);  // bytes past the batch read 0
         }
         // ---- move, part 1: this iteration's bytes of the current token (rem == 0: nothing);
@@ -173,9 +200,27 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         i = np ? i + adv : i;
         // the next header (lanes not parsing reload theirs), one load for every lane: near the
         // batch's end from its last 16 bytes, shifted after the wait at the next iteration's top
-        const uint8_t *hc = b + i > in_end - 16 ? in_end - 16 : b + i;  // (the batch's last 16 bytes)
-        h = ld16v(hc);
-        hd = (int32_t)(b + i - hc);
+        if (HW) {
+            const uint8_t *y = b + i;
+            const bool rl = y > wb + 16;  // (the header leaves the window; i never moves back)
+            if (any_lane(rl)) {
+                if (rl) {
+                    wb = (const uint8_t *)((uintptr_t)y & ~(uintptr_t)15);
+                    if (wb >= A.in && wb + 32 <= in_end) {
+                        hw0 = ld16v(wb);
+                        hw1 = ld16v(wb + 16);
+                    } else {  // the batch's end: bytes past it read 0
+                        hw0 = ld_clamped16(wb, A.in, in_end);
+                        hw1 = ld_clamped16(wb + 16, A.in, in_end);
+                    }
+                }
+            }
+            hd = (int32_t)(y - wb);
+        } else {
+            const uint8_t *hc = b + i > in_end - 16 ? in_end - 16 : b + i;  // (the batch's last 16 bytes)
+            h = ld16v(hc);
+            hd = (int32_t)(b + i - hc);
+        }
         // ---- move, part 2
         V16 g = graw;
         if (any_lane(hb && gd != 0)) {  // bytes outside the batch or before the slot read 0
@@ -252,6 +297,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
 
 // spw: streams per wave (lanes spw..63 idle): fewer streams per wave put more
 // waves on each SIMD within the same LDS
+template <bool HW>
 __global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A, uint32_t spw, uint32_t fper) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint32_t l = threadIdx.x & 63, w = threadIdx.x >> 6;
@@ -259,7 +305,7 @@ __global__ __launch_bounds__(kRingBlock) void k2_ring(DecompressArgs A, uint32_t
     uint8_t *ring = smem + (w * spw + l) * kRingStride + 16;
     const uint64_t per_block = (uint64_t)(kRingBlock / 64) * spw;
     for (uint64_t s = (uint64_t)blockIdx.x * per_block + w * spw + l; s < A.count; s += (uint64_t)gridDim.x * per_block)
-        if (!ring_one(A, s, ring, fper)) {
+        if (!ring_one<HW>(A, s, ring, fper)) {
             const uint32_t at = atomicAdd(&A.slow[0], 1u);
             A.slow[1 + at] = (uint32_t)s;
         }
@@ -272,9 +318,11 @@ hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t st) {
     static bool attr_done = false;
     const size_t lds = (size_t)(kRingBlock / 64) * spw * kRingStride;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k2_ring, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k2_ring<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k2_ring<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
+    static const bool hw = knob("EZ_K2R_HW", 1) != 0;  // A/B (experiment builds): the aligned header window
     const uint64_t per_block = (uint64_t)(kRingBlock / 64) * spw;
     const uint64_t grid = (a.count + per_block - 1) / per_block;
     // EZ_K2R_FLUSH (A/B): iterations between ring flushes, a power of two <= kMaxFlushPer
@@ -282,7 +330,8 @@ hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t st) {
         const uint32_t v = (uint32_t)knob("EZ_K2R_FLUSH", 8);
         return v >= 1 && v <= kMaxFlushPer && (v & (v - 1)) == 0 ? v : 8u;
     }();
-    hipLaunchKernelGGL(k2_ring, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a, spw, fper);
+    if (hw) hipLaunchKernelGGL(k2_ring<true>, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a, spw, fper);
+    else hipLaunchKernelGGL(k2_ring<false>, dim3((unsigned)grid), dim3(kRingBlock), lds, st, a, spw, fper);
     return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@ package eazy
 import (
 	"bytes"
 	"io"
+	"runtime"
 	"testing"
 )
 
@@ -86,4 +87,53 @@ func TestErrorText(t *testing.T) {
 	expectPanic("too big length", func() { Encoder{}.Tag(nil, Literal, 0x1_1000_0000) })
 	expectPanic("too big offset", func() { Encoder{}.Offset(nil, 0x1_1000_0000, 10) })
 	expectPanic(1024, func() { Encoder{}.Meta(nil, 1024, 4) })
+}
+
+// Dump's text on the TestCopy stream (block 32, htable 16, no magic), whole and cut inside the
+// second literal: the expected strings are eazy_amd/dump.py's (the C++ mirror prints the same,
+// tests/test_cpp.py), which restates the reference's format (reader.go:602-732).
+func TestDump(t *testing.T) {
+	var buf bytes.Buffer
+	w := NewWriter(&buf, 32, 16)
+	w.AppendMagic = false
+	w.Write([]byte("prefix_1234_suffix"))
+	w.Write([]byte("prefix_567_suffix"))
+	c := buf.Bytes()
+	want := "     0     0       0  meta  2 1  \"\\x05\"    05\n" +
+		"     3     3       0  lit    12        \"prefix_1234_suffix\"\n" +
+		"    16    16      12  copy    7  off   12\n" +
+		"    18    18      19  lit     3        \"567\"\n" +
+		"    1c    1c      1c  copy    7  off   11\n" +
+		"    1e     0      23  "
+	if got := Dump(c); got != want {
+		t.Fatalf("Dump:\n%q\nwant\n%q", got, want)
+	}
+	cut := "     0     0       0  meta  2 1  \"\\x05\"    05\n" +
+		"     3     3       0  lit    12        \"prefix_1234_suffix\"\n" +
+		"    16    16      12  copy    7  off   12\n" +
+		"    18    18      19      19     0      19  \nerror: short buffer"
+	if got := Dump(c[:len(c)-3]); got != cut {
+		t.Fatalf("Dump (cut):\n%q\nwant\n%q", got, cut)
+	}
+}
+
+// Writers and Readers that are never closed (the reference has no Close) give their device
+// memory back when collected: 256 handles with 4 MiB rings would hold 1 GiB of HBM otherwise.
+func TestHandlesFreedWithoutClose(t *testing.T) {
+	p := bytes.Repeat([]byte("ts=3 level=info msg=\"ok\" "), 160)
+	for k := 0; k < 256; k++ {
+		var buf bytes.Buffer
+		w := NewWriter(&buf, 4*MiB, 4096)
+		if _, err := w.Write(p); err != nil {
+			t.Fatal(err)
+		}
+		r := NewReaderBytes(buf.Bytes())
+		q := make([]byte, len(p))
+		if n, err := io.ReadFull(r, q); err != nil || n != len(p) || !bytes.Equal(q, p) {
+			t.Fatalf("round trip %d: %v", k, err)
+		}
+		if k%32 == 31 {
+			runtime.GC()
+		}
+	}
 }

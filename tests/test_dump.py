@@ -6,6 +6,8 @@ test_dump_runlen_kat is derived by hand from the format verbs of
 reader.go:622-700 (the reference's tests only log dumps: the text is parity
 unpinned).  CPU only: the token decoders are host code of libeazy_amd.so."""
 
+import os
+
 import oracle as orc
 from golden_data import h, load
 
@@ -164,3 +166,25 @@ def test_dumper_synthetic_streams():
         d2 = Dumper()
         assert d2.ReadFrom(Src()) == (len(s), 0)
         assert d2.pos == len(raw)
+
+
+def test_dump_text_go_test_strings():
+    """The expected texts go/eazy/eazy_test.go's TestDump carries (uncompiled here: no Go
+    toolchain) are what the Python mirror prints for that stream, whole and cut."""
+    import re
+
+    from eazy_amd import dump
+
+    c = orc.compress(32, 16, [b"prefix_1234_suffix", b"prefix_567_suffix"], append_magic=False)
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "go", "eazy", "eazy_test.go")).read()
+    body = src[src.index("func TestDump"):src.index("func TestHandlesFreedWithoutClose")]
+
+    lit = r'"((?:[^"\\]|\\.)*)"'
+
+    def go_string(var):
+        start = body.index(var + " := ") + len(var) + 4
+        end = body.index("\n\tif ", start)
+        return "".join(p.encode().decode("unicode_escape") for p in re.findall(lit, body[start:end]))
+
+    assert dump.Dump(c) == go_string("want")
+    assert dump.Dump(c[:-3]) == go_string("cut")

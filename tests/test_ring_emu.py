@@ -28,13 +28,18 @@ def emu():
     return EMU
 
 
-def _run(emu, tmp_path, bufs, block=1 << 20, htable=1024):
+@pytest.fixture(params=[1, 0], ids=["header-window", "header-per-token"])
+def hw(request):
+    return request.param
+
+
+def _run(emu, tmp_path, bufs, block=1 << 20, htable=1024, hw=1):
     comp = [orc.compress(block, htable, [b]) for b in bufs]
     offs = np.concatenate([[0], np.cumsum([len(c) for c in comp])]).astype(np.uint64)
     cap = max(16, max(len(b) for b in bufs))
     (tmp_path / "in").write_bytes(b"".join(comp))
     (tmp_path / "off").write_bytes(offs.tobytes())
-    subprocess.run([emu, str(tmp_path / "in"), str(tmp_path / "off"), str(cap), str(tmp_path / "out"), str(tmp_path / "sz")],
+    subprocess.run([emu, str(tmp_path / "in"), str(tmp_path / "off"), str(cap), str(tmp_path / "out"), str(tmp_path / "sz"), str(hw)],
                    check=True, timeout=600)
     out = (tmp_path / "out").read_bytes()
     sz = np.frombuffer((tmp_path / "sz").read_bytes(), np.uint64)
@@ -45,22 +50,22 @@ def _run(emu, tmp_path, bufs, block=1 << 20, htable=1024):
         at += int(sz[s])
 
 
-def test_logs(emu, tmp_path):
+def test_logs(emu, tmp_path, hw):
     from eazy_amd import synth
 
     d = synth.logs(3, 256 * 4096).tobytes()
-    _run(emu, tmp_path, [d[k * 4096 : (k + 1) * 4096] for k in range(256)])
+    _run(emu, tmp_path, [d[k * 4096 : (k + 1) * 4096] for k in range(256)], hw=hw)
 
 
-def test_long_streams(emu, tmp_path):
+def test_long_streams(emu, tmp_path, hw):
     """Streams much longer than the ring: far copies read the flushed output."""
     from eazy_amd import synth
 
     d = synth.logs(5, 4 << 20).tobytes()
-    _run(emu, tmp_path, [d[: 1 << 20], d[1 << 20 : (1 << 20) + 100003], d[3 << 20 :]])
+    _run(emu, tmp_path, [d[: 1 << 20], d[1 << 20 : (1 << 20) + 100003], d[3 << 20 :]], hw=hw)
 
 
-def test_edges_random_runs(emu, tmp_path):
+def test_edges_random_runs(emu, tmp_path, hw):
     from eazy_amd import synth
 
     rng = np.random.default_rng(11)
@@ -85,4 +90,4 @@ def test_edges_random_runs(emu, tmp_path):
             z[idx] = rng.integers(1, 256, len(idx), dtype=np.uint8)
             b = z.tobytes()
         bufs.append(b)
-    _run(emu, tmp_path, bufs)
+    _run(emu, tmp_path, bufs, hw=hw)

@@ -21,6 +21,7 @@ static std::vector<uint8_t> slurp(const char *f) {
 
 int main(int argc, char **argv) {
     if (argc < 6) return 2;
+    const bool hw = argc < 7 || atoi(argv[6]) != 0;  // the aligned header window (default) or the per-token load
     auto in = slurp(argv[1]);
     auto ob = slurp(argv[2]);
     const uint64_t *offs = (const uint64_t *)ob.data();
@@ -39,7 +40,7 @@ int main(int argc, char **argv) {
     a.count = count;
     alignas(16) static uint8_t ring[1024];
     for (uint64_t s = 0; s < count; s++)
-        if (!ez::ring_one(a, s, ring + 16)) size[s] = ~0ull;  // front guard
+        if (!(hw ? ez::ring_one<true>(a, s, ring + 16) : ez::ring_one<false>(a, s, ring + 16))) size[s] = ~0ull;  // front guard
     FILE *fo = std::fopen(argv[4], "wb");
     for (uint64_t s = 0; s < count; s++)
         if (size[s] != ~0ull) std::fwrite(out.data() + out_off[s], 1, size[s], fo);
