@@ -314,11 +314,12 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
                                : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : (v && strcmp(v, "small") == 0 ? 's' : 0)));
     }
     const uint64_t exact_grid = a.count < 4096 ? a.count : 4096;
-    // Slots of at most 4 KiB (C1, C3) go to K2s; up to 64 KiB to K2r's lane per stream; longer ones (C2,
-    // C4, the sweep's long streams) to K2t (1 GiB batches, K2 ms, K2r / K2t: 8 KiB 1.89 / 4.99, 16 KiB
-    // 1.96 / 4.89, 32 KiB 3.50 / 5.06, 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5)
-    // - / 7.0, 1 MiB (K2w 29.7) - / 14.4; C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms)
-    const int v = g_decompress_variant != 0 ? g_decompress_variant : (a.max_out <= (uint64_t)kSmallOut ? 's' : (a.max_out >= long_slot ? 't' : 'r'));
+    // Slots under 64 KiB go to K2r's lane per stream; longer ones (C2, C4, the sweep's long streams) to
+    // K2t (1 GiB batches, K2 ms, K2r / K2t: 8 KiB 1.89 / 4.99, 16 KiB 1.96 / 4.89, 32 KiB 3.50 / 5.06,
+    // 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5) - / 7.0, 1 MiB (K2w 29.7) - / 14.4;
+    // C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms).  K2s (slots <= 4 KiB) is reached only when
+    // forced: at C1 it measured 1.15 ms against K2r's 0.46.
+    const int v = g_decompress_variant != 0 ? g_decompress_variant : (a.max_out >= long_slot ? 't' : 'r');
     g_last_variant = v;
     if (v == 's') {
         // K2s: the token walk writes each stream's bitmap of token starts (or hands it over), the move

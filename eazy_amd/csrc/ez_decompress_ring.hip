@@ -100,10 +100,10 @@ __host__ __device__ __forceinline__ V16 win16(V16 a, V16 b, uint32_t o) {
 // decodes stream s with `ring` (kRing + 16 bytes, with 16-byte guards on both sides) as its history; false = hand
 // the stream over (host-compilable: tools/ring_emu.hip runs it on the CPU)
 // fper: iterations between flushes (a power of two <= kMaxFlushPer)
-// HW: the headers come from a 32-byte window of 16-byte-aligned input loads, reloaded only when the
-// next header leaves it (a token takes ~5 input bytes at C1: one aligned pair per ~3 tokens, each
-// 16-byte aligned load one access of the vector memory path), instead of one byte-unaligned 16-byte
-// load (one access per dword it touches) per token
+// HW (A/B only): the headers from a 32-byte window of 16-byte-aligned input loads, reloaded only when
+// the next header leaves it (one aligned pair per ~3 tokens at C1), instead of one byte-unaligned
+// 16-byte load per token: measured slower at C1 (0.544 against 0.462 ms): the loads are not what
+// binds K2r, and the window's selects and the reload branch add to the per-token chain
 template <bool HW>
 __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const uint64_t s, uint8_t *ring, uint32_t fper = 8) {
     const uint8_t *b = A.in + A.in_off[s];
@@ -322,7 +322,7 @@ hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t st) {
         (void)hipFuncSetAttribute((const void *)k2_ring<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
-    static const bool hw = knob("EZ_K2R_HW", 1) != 0;  // A/B (experiment builds): the aligned header window
+    static const bool hw = knob("EZ_K2R_HW", 0) != 0;  // A/B (experiment builds): the aligned header window
     const uint64_t per_block = (uint64_t)(kRingBlock / 64) * spw;
     const uint64_t grid = (a.count + per_block - 1) / per_block;
     // EZ_K2R_FLUSH (A/B): iterations between ring flushes, a power of two <= kMaxFlushPer

@@ -146,9 +146,10 @@ __device__ __forceinline__ void refill_commit(const Refill &r, uint8_t *ring, ui
             const int x = 4 * k + q;
             w[q] = swar_step(d[x], __builtin_amdgcn_alignbyte(d[x + 1], d[x], 1));
         }
-        const int32_t slot = (at - 8 + 16 * k) & (kPRing - 1);
-        *(u64_ua *)(tab + slot) = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
-        *(u64_ua *)(tab + slot + 8) = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
+        // (8-byte pieces at 8-aligned slots: at - 8 + 16 k is 8 mod 16, so a 16-byte store at the
+        // last slot would run past the lane's table)
+        *(uint64_t *)(tab + ((at - 8 + 16 * k) & (kPRing - 1))) = (uint64_t)w[0] | ((uint64_t)w[1] << 32);
+        *(uint64_t *)(tab + ((at + 16 * k) & (kPRing - 1))) = (uint64_t)w[2] | ((uint64_t)w[3] << 32);
     }
 }
 

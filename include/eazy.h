@@ -216,7 +216,7 @@ int ez_select_compress_kernel(int kind);
  * workspace ('s' a token-walk kernel then 16 lanes per stream with the whole output in LDS, for
  * slots of at most 4 KiB; 'r' lane-per-stream with an LDS ring of recent output, 't'
  * token-parallel wave per stream, 'w' wave per stream with a scalar token walk; 0 = automatic:
- * 's' when every slot is at most 4 KiB, 't' when one is 64 KiB or more, else 'r'; the largest
+ * 't' when a slot is 64 KiB or more, else 'r' ('s' only when forced); the largest
  * slot is max_len when the caller gives it, else measured on the device, which waits for the
  * stream).  Streams the chosen kernel cannot take go on to the exact decoder. */
 int ez_select_decompress_kernel(int kind);

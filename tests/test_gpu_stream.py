@@ -457,3 +457,64 @@ def test_handle_writes_k1l_and_general(cuda, block, ht):
     want = orc.compress(block, ht, writes)
     assert outs[0] == want, "K1L handle path"
     assert outs[1] == want, "general kernel"
+
+
+def test_k2s_checks_and_forms(cuda):
+    """K2s (the token walk + the 16-lane move kernel) on hand-built small streams: every check
+    the move kernel makes hands the stream to the exact decoder with the reference's result —
+    slots one byte too small, BlockSizeLimit below a token's length, a copy farther than the
+    window (MetaReset with a 32-byte block), a token before the window is set, a reset after
+    output — and the long forms it parses itself (Len1/Len2 literals and copies, Off1/Off2/
+    OffLong offsets, zero regions, short-period runs, copies reaching before the stream start).
+    Statuses, sizes and bytes equal the oracle's for every slot size and limit."""
+    import torch
+
+    import eazy_amd as ez
+    import oracle as orc
+
+    rng = np.random.default_rng(11)
+    hdr = b"\x80\x02eazy\x80\x10\x14"  # magic, reset to a 1 MiB block (reader.go continueMetaTag)
+
+    def lit(b):
+        return _tag(0x00, len(b)) + b
+
+    def cpy(d, n, lng=False):  # a distance below the length (a run) takes the OffLong form, as Encoder.Offset
+        return _tag(0x80, n) + (b"\xff" + _off(d, 0) if lng or d < n else _off(d, n))
+
+    good = []
+    # long forms: Len1 / Len2 literals, Len1 copies, Off1 / Off2 offsets, OffLong, zero region, runs
+    a = rng.integers(0, 256, 300, dtype=np.uint8).tobytes()
+    good.append(hdr + lit(a) + cpy(300, 200) + cpy(250, 130) + lit(b"x") + cpy(1, 40) + cpy(3, 33) + cpy(0, 100))
+    b = rng.integers(97, 100, 700, dtype=np.uint8).tobytes()
+    good.append(hdr + lit(b) + cpy(600, 500, lng=True) + cpy(509, 60) + cpy(253, 7) + lit(b"tail"))
+    good.append(hdr + cpy(0, 64) + cpy(2000, 30) + lit(b"abc") + cpy(5, 9))  # zero history before the start
+    good.append(hdr + b"\x00\x00\x00" + lit(b"pad") + b"\x00" + b"\x80\x1f" + cpy(3, 12))  # padding and a break
+    bad = [
+        b"\x80\x02eazy\x80\x10\x05" + lit(rng.integers(0, 256, 40, dtype=np.uint8).tobytes()) + cpy(36, 8),  # D > 32-byte window
+        lit(b"no reset first") + hdr,  # a token before the window is set
+        hdr + lit(b"abcdef") + b"\x80\x10\x14" + cpy(3, 4),  # a reset after output
+    ]
+    ins = good + bad
+    lens = [len(orc.decompress(x, cap=1 << 20)[0]) for x in ins]
+    offs = np.concatenate([[0], np.cumsum([len(x) for x in ins])]).astype(np.int64)
+    comp = torch.from_numpy(np.frombuffer(b"".join(ins) + bytes(64), np.uint8).copy()).to(cuda)
+    coff = torch.from_numpy(offs).to(cuda)
+    for cap, limit in ((4096, 0), (max(lens), 0), (max(lens) - 1, 0), (4096, 64), (4096, 250)):
+        ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
+        res = {}
+        for kind in ("s", ""):
+            ez.select_decompress_kernel(kind)
+            try:
+                res[kind] = ez.decompress_batch(comp, coff, ooff, block_size_limit=limit, max_len=cap)
+                torch.cuda.synchronize()
+            finally:
+                ez.select_decompress_kernel("")
+        ex = ez.decompress_batch(comp, coff, ooff, block_size_limit=limit, exact_only=True)
+        torch.cuda.synchronize()
+        for kind, (out, sizes, status) in res.items():
+            assert torch.equal(status, ex[2]) and torch.equal(sizes, ex[1]), (kind, cap, limit)
+            for s in range(len(ins)):
+                n = int(sizes[s])
+                assert torch.equal(out[s * cap : s * cap + n], ex[0][s * cap : s * cap + n]), (kind, cap, limit, s)
+        if limit == 0:
+            _cmp_oracle(ins, cap, res["s"][0].cpu().numpy(), res["s"][1].cpu().numpy(), res["s"][2].cpu().numpy())
