@@ -114,6 +114,8 @@ def _lib():
     L.ez_writer_reset_size.argtypes = [vp, i64, i64]
     L.ez_writer_is_reset.argtypes = [vp]
     L.ez_writer_last_panic.argtypes = [vp]
+    L.ez_reader_set_whole.argtypes = [vp, C.c_int]
+    L.ez_reader_whole_decoded.argtypes = [vp]
     L.ez_writer_size_panic.argtypes = [i64, i64]
     L.ez_panic_message.restype = C.c_char_p
     L.ez_panic_message.argtypes = [C.c_int]
@@ -429,6 +431,7 @@ class Reader:
         h = C.c_void_p()
         _check(_lib().ez_reader_new(device, C.byref(h)))
         self._h = h
+        _lib().ez_reader_set_whole(h, 0 if r is not None else 1)  # a whole buffer: decoded at once
         self.Reader = r
         self._b = bytearray(b or b"")
         self._i = 0
@@ -447,6 +450,7 @@ class Reader:
     def Reset(self, rd) -> None:  # reader.go:96-99
         self.ResetBytes(b"")
         self.Reader = rd
+        _lib().ez_reader_set_whole(self._h, 0)
 
     def ResetBytes(self, b: bytes) -> None:  # reader.go:102-113
         self.Reader = None
@@ -454,6 +458,12 @@ class Reader:
         self._i = 0
         self._boff = 0
         _lib().ez_reader_reset(self._h)
+        _lib().ez_reader_set_whole(self._h, 1)
+
+    @property
+    def whole_decoded(self) -> bool:
+        """True while the Reads are served from the whole-stream decode (ez_reader_whole_decoded)."""
+        return bool(_lib().ez_reader_whole_decoded(self._h))
 
     def Read(self, n: int):  # reader.go:116-141
         L = _lib()

@@ -345,13 +345,16 @@ class Reader {
     void Reset(IoReader *r) {  // reader.go:96-99
         ResetBytes(nullptr, 0);
         R = r;
+        ez_reader_set_whole(h_, 0);
     }
+    // (a whole buffer: the handle decodes it at once on the first Read, ez_reader_set_whole)
     void ResetBytes(const uint8_t *b, size_t n) {  // reader.go:102-113
         R = nullptr;
         b_.assign(b, b + n);
         i_ = 0;
         boff_ = 0;
         ez_reader_reset(h_);
+        ez_reader_set_whole(h_, 1);
     }
     void ResetBytes(const std::vector<uint8_t> &b) { ResetBytes(b.data(), b.size()); }
 

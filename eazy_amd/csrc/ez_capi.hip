@@ -598,6 +598,13 @@ struct ez_reader {
     DBuf in, obuf[2], dstate, meta;  // obuf: history + output, double-buffered (ez_reader_read)
     int cur = 0;
     hipStream_t stream = nullptr;
+    // whole-buffer decode-ahead (ez_reader_set_whole): the stream decoded once by the batch path,
+    // the Reads served from `ahead`
+    int whole = 0;          // the caller's b is the whole stream (NewReaderBytes / ResetBytes)
+    int tried = 0;          // decode-ahead tried since the last reset
+    int ahead_on = 0;       // Reads are served from ahead[ahead_at .. ahead.size())
+    std::vector<uint8_t> ahead;
+    size_t ahead_at = 0;
 };
 
 extern "C" int ez_reader_new(int device, ez_reader **out) {
@@ -643,10 +650,79 @@ extern "C" int ez_reader_reset(ez_reader *r) {
     const int32_t ver = r->st.ver;
     r->st = ez::DecodeState{};
     r->st.ver = ver;
+    r->tried = 0;
+    r->ahead_on = 0;
+    r->ahead.clear();
+    r->ahead.shrink_to_fit();
+    r->ahead_at = 0;
     return EZ_OK;
 }
 
+extern "C" int ez_reader_set_whole(ez_reader *r, int whole) {
+    r->whole = whole ? 1 : 0;
+    return EZ_OK;
+}
+
+extern "C" int ez_reader_whole_decoded(const ez_reader *r) { return r->ahead_on; }
+
 extern "C" int ez_reader_pending(const ez_reader *r) { return r->st.state != 0 ? 1 : 0; }
+
+namespace {
+// Decode-ahead of a whole stream (NewReaderBytes then Read to the end, the reference's common use):
+// the batch path decodes b as one stream -- K2t, every lane of a wave on its tokens -- into a slot of
+// up to 8 x b_len bytes, and the Reads are then served from that output.  It applies only where Read
+// by Read decoding gives exactly those bytes and nothing else: a clean end of stream (status OK) and
+// no Break meta (Read reports ErrBreak there, the batch path skips it), with RequireMagic and
+// SkipUnsupportedMeta off; anything else leaves the handle as it was and the exact decoder runs Read
+// by Read.  Returns 1 when the Reads are now served from the decoded bytes.
+int reader_ahead(ez_reader *r, const uint8_t *b, size_t b_len) {
+    r->tried = 1;
+    if (b_len == 0 || b_len > ((size_t)1 << 28) || r->require_magic || r->skip_meta) return 0;
+    const size_t cap = 8 * b_len + 4096 < ((size_t)1 << 30) ? 8 * b_len + 4096 : ((size_t)1 << 30);
+    DBuf din, dout, dm, dws;
+    const size_t ws = ez_decompress_workspace(1);
+    const size_t o_meta = 64;
+    if (din.ensure(b_len + 64) || dout.ensure(cap + 64) || dm.ensure(o_meta + 8 * 8) || dws.ensure(ws)) return 0;
+    uint64_t m[8] = {0, (uint64_t)b_len, 0, (uint64_t)cap, 0, 0, 0, 0};  // in_off, out_off, out_size, status, breaks
+    int ok = 0;
+    do {
+        if (hipMemcpyAsync(din.p, b, b_len, hipMemcpyHostToDevice, r->stream) != hipSuccess) break;
+        if (hipMemcpyAsync(dm.p, m, sizeof m, hipMemcpyHostToDevice, r->stream) != hipSuccess) break;
+        uint64_t *dmw = dm.as<uint64_t>();
+        ez::DecompressArgs a{};
+        a.in = din.as<uint8_t>();
+        a.in_off = dmw;
+        a.out = dout.as<uint8_t>();
+        a.out_off = dmw + 2;
+        a.out_size = dmw + 4;
+        a.status = (int32_t *)(dmw + 5);
+        a.breaks = (uint32_t *)(dmw + 6);
+        a.count = 1;
+        a.block_size_limit = r->limit;
+        a.slow = dws.as<uint32_t>();
+        a.max_out = cap;
+        a.force = 't';  // one stream: the token-parallel wave
+        if (ez::launch_decompress(a, r->stream) != hipSuccess) break;
+        if (hipMemcpyAsync(m, dm.p, sizeof m, hipMemcpyDeviceToHost, r->stream) != hipSuccess) break;
+        if (hipStreamSynchronize(r->stream) != hipSuccess) break;
+        if ((int32_t)(m[5] & 0xffffffffu) != EZ_OK || (uint32_t)m[6] != 0 || m[4] > cap) break;
+        r->ahead.resize((size_t)m[4]);
+        if (m[4] && hipMemcpy(r->ahead.data(), dout.p, (size_t)m[4], hipMemcpyDeviceToHost) != hipSuccess) break;
+        r->ahead_at = 0;
+        r->ahead_on = 1;
+        ok = 1;
+    } while (0);
+    if (!ok) {
+        r->ahead.clear();
+        r->ahead.shrink_to_fit();
+    }
+    din.release();
+    dout.release();
+    dm.release();
+    dws.release();
+    return ok;
+}
+}  // namespace
 
 // Input is uploaded in windows from b[i] on, not the whole of b per call: a Read loop over one large
 // NewReaderBytes buffer then moves each input byte to the device about once.  A window that ends inside
@@ -663,6 +739,18 @@ extern "C" int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size
     if (p_len == 0) return EZ_OK;  // Read(p) with len(p) == 0 returns at once (reader.go:119)
     DeviceGuard g(r->device);
     if (!g.ok) return EZ_EDEVICE;
+    // a fresh handle over a whole stream: decode it once (reader_ahead), then serve every Read from it
+    if (!r->ahead_on && r->whole && !r->tried && i == 0 && boff == 0 && r->st.bs == 0 && r->st.pos == 0 && r->st.state == 0)
+        (void)reader_ahead(r, b, b_len);
+    if (r->ahead_on) {
+        const size_t left = r->ahead.size() - r->ahead_at, m = p_len < left ? p_len : left;
+        if (m) memcpy(p, r->ahead.data() + r->ahead_at, m);
+        r->ahead_at += m;
+        *n = m;
+        if (m == p_len) return EZ_OK;  // (the input position is reported when the output is done)
+        *i_out = b_len;                 // the stream's end: Read asks for more input and gets EOF
+        return EZ_ESHORTBUF;
+    }
     const size_t H = (size_t)r->st.hist;
     DBuf &cur = r->obuf[r->cur];
     if (cur.cap < H + p_len + 16) {  // grow, keeping the history at the head

@@ -706,8 +706,9 @@ __device__ __forceinline__ void lds_put12(uint64_t *tab, uint32_t h, uint32_t va
     asm volatile("ds_mskor_b64 %0, %1, %2" : : "v"(addr), "v"(m), "v"(v) : "memory");
 }
 
-// TB: the table's visit -- 0 the DPP search over a u16 table, 16 lds_mskor16, 12 lds_mskor12
-template <int TB>
+// TB: the table's visit -- 0 the DPP search over a u16 table, 16 lds_mskor16, 12 lds_mskor12;
+// NT: the records are stored nontemporal (read back by another kernel) or plain (by this wave)
+template <int TB, bool NT = true>
 __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int32_t n, int lj, int g, uint16_t *hth,
                                           uint32_t hsh, uint64_t *recw, uint32_t roff, uint64_t rcap, int prio, int32_t &nrec_out,
                                           int &err) {
@@ -839,7 +840,10 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
                 else hth[h1] = (uint16_t)(x + 1);
             }
 #if !(EZ_EXP & 32768)
-            if ((uint64_t)nrec < rcap) __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), recw + (roff + (uint32_t)nrec));
+            if ((uint64_t)nrec < rcap) {
+                if (NT) __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), recw + (roff + (uint32_t)nrec));
+                else recw[roff + (uint32_t)nrec] = rec_pack(lit, nx - lit, dist, force);
+            }
 #else  // (timing builds: the records' traffic without their lines -- k1_emit then sees none)
             __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), recw + (roff + (uint32_t)(nrec & 1)));
 #endif
@@ -1429,7 +1433,12 @@ constexpr int32_t kEdgeBefore = 64;  // readable bytes before a stream (WinRoll'
 __host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + kEdgeBefore + 64 + 15) & ~15ull; }
 __host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs &a) { return 128 + kEdgeSlots * edge_slot_bytes(a) + 16; }
 
-template <int TB>
+template <bool WIDE>
+__device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane);
+
+// FUSE: the wave writes its four streams' tokens itself after the parse (emit_stream, one stream at a
+// time by the whole wave), instead of a separate k1_emit launch reading the records back
+template <int TB, bool FUSE = false>
 __global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                  uint64_t rcap, int prio, uint8_t *edge) {
     constexpr int G = 16, S = 64 / G;
@@ -1475,8 +1484,18 @@ __global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, 
         __threadfence_block();
     }
     int32_t nrec = 0;
-    lean_loop<TB>(LeanIn{}, p, n, lj, g, hth, hsh, recw, roff, rcap, prio, nrec, err);
+    lean_loop<TB, !FUSE>(LeanIn{}, p, n, lj, g, hth, hsh, recw, roff, rcap, prio, nrec, err);
     if (have && lj == 0) A.out_size[s] = (uint64_t)((EZ_EXP & 32768) ? 0 : nrec) | ((uint64_t)err << 48);
+    if (FUSE) {
+        // the records and counts this wave stored, visible to all its lanes (one wave, one CU: its
+        // stores complete, then its loads read them through the same L1)
+        __builtin_amdgcn_s_waitcnt(0);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+        for (int q = 0; q < S; q++) {
+            const uint64_t sq = (uint64_t)blockIdx.x * S + (uint64_t)q;
+            if (sq < A.count) emit_stream<false>(A, recs, rcap, sq, lane);
+        }
+    }
 }
 
 // ---------------------------------------------------------------- K1e
@@ -1497,12 +1516,9 @@ constexpr int32_t kLongLit = 96;  // literals this long are copied by the whole 
 // WIDE: k1_long's 16-byte records, and (spec_mode) the streams K1x hands over: their header and
 // first tokens are written already, the output continues at spec[s].op with the pending literal
 // from spec[s].done; streams K1x finished are skipped
+// the token writer of stream s (wave-uniform) by one wave
 template <bool WIDE>
-__global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t *recs, uint64_t rcap) {
-    const int lane = (int)(threadIdx.x & 63);
-    // the wave's stream, wave-uniform (readfirstlane: its per-stream values live in SGPRs)
-    const uint64_t s = (uint64_t)blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (s >= A.count) return;
+__device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane) {
     const bool spec = WIDE && A.spec_mode != 0;
     if (spec && A.spec[s].flags != 0) return;
     const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
@@ -1636,6 +1652,15 @@ __global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t
     }
 }
 
+template <bool WIDE>
+__global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t *recs, uint64_t rcap) {
+    const int lane = (int)(threadIdx.x & 63);
+    // the wave's stream, wave-uniform (readfirstlane: its per-stream values live in SGPRs)
+    const uint64_t s = (uint64_t)blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (s >= A.count) return;
+    emit_stream<WIDE>(A, recs, rcap, s, lane);
+}
+
 // LDS words of a stream's table (0 = this variant cannot take the batch)
 template <bool T16>
 uint32_t split_table_words(const CompressArgs &a) {
@@ -1723,6 +1748,17 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     if (z != hipSuccess) return z;
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
     static const size_t pad = (size_t)knob("EZ_K1S_LDSPAD", 0);
+    // EZ_K1S_FUSE=1 (A/B): the token writer inside the parse kernel
+    static const bool fuse = knob("EZ_K1S_FUSE", 0) != 0;
+    if (fuse && msk && !t12) {
+        static bool fattr = false;
+        if (!fattr) {
+            (void)hipFuncSetAttribute((const void *)k1_lean<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            fattr = true;
+        }
+        hipLaunchKernelGGL((k1_lean<16, true>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
+        return hipGetLastError();
+    }
     if (t12)
         hipLaunchKernelGGL(k1_lean<12>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
     else if (msk)

@@ -223,6 +223,7 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
                 if (m > 0) { err = EZ_ENOSPC; break; }
             }
             total += m;
+            if (err == EZ_EBREAK && A.breaks && lane == 0) atomicAdd(A.breaks, 1u);
             if (err == EZ_OK || err == EZ_EBREAK) continue;
             if (err == EZ_ESHORTBUF) err = (d.state != 0 || i < d.nb) ? EZ_EUNEXPECTEDEOF : EZ_OK;
             break;
@@ -319,7 +320,7 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     // 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5) - / 7.0, 1 MiB (K2w 29.7) - / 14.4;
     // C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms).  K2s (slots <= 4 KiB) is reached only when
     // forced: at C1 it measured 1.15 ms against K2r's 0.46.
-    const int v = g_decompress_variant != 0 ? g_decompress_variant : (a.max_out >= long_slot ? 't' : 'r');
+    const int v = a.force ? a.force : (g_decompress_variant != 0 ? g_decompress_variant : (a.max_out >= long_slot ? 't' : 'r'));
     g_last_variant = v;
     if (v == 's') {
         // K2s: the token walk writes each stream's bitmap of token starts (or hands it over), the move

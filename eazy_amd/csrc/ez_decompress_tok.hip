@@ -134,9 +134,11 @@ __device__ __forceinline__ int32_t run_step_of(int32_t per) { return per * (16 /
 
 // the advance of a rare form at input position p (h: its 16 bytes, the same on every lane):
 // the full parse; 2^30 (past any stream) when the stream goes to the exact decoder
-__device__ __attribute__((noinline)) int32_t rare_adv(const uint8_t *h, int32_t p, int32_t nb, int32_t lim32, int64_t limit) {
+__device__ __attribute__((noinline)) int32_t rare_adv(const uint8_t *h, int32_t p, int32_t nb, int32_t lim32, int64_t limit, uint32_t *brk) {
     K2Tok t;
     const int rr = k2_scan(lds16<0>(h), p, nb, lim32, limit, t);
+    // a Break meta (0x80, MetaBreak | MetaLen0): counted for the callers that must see it (Reader handles)
+    if (brk && rr == kParseSkip && h[0] == 0x80 && h[1] == (kMetaBreak | kMetaLen0) && threadIdx.x == 0) atomicAdd(brk, 1u);
     return __builtin_amdgcn_readfirstlane(rr == kParseHandOver ? (1 << 30) : t.adv);
 }
 
@@ -252,7 +254,7 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
             }
             int32_t x = __builtin_amdgcn_readfirstlane((int32_t)ex[e]);
             if (x == e) {  // a rare form: the full parse (2^30: hand over)
-                x = e + __builtin_amdgcn_readfirstlane(rare_adv(inb + e, base + e, nb, lim32, limit));
+                x = e + __builtin_amdgcn_readfirstlane(rare_adv(inb + e, base + e, nb, lim32, limit, A.breaks));
                 if (lane == 0) ex[e] = (uint16_t)(x < 0xffff ? x : 0xffff);
             }
             e = x;

@@ -111,6 +111,8 @@ struct DecompressArgs {
     uint64_t defer_cap;       // records reserved
     uint64_t max_out;         // batch: host hint, largest output slot (0 = unknown)
     const uint32_t *todo;     // batch: [0] = count, [1..] = the streams to decode (nullptr = all)
+    uint32_t *breaks;         // batch, optional: counts the Break metas the decoders skip (reader.go:306-307)
+    int force;                // batch: the first K2 kernel ('r', 't', ...; 0 = the automatic / selected one)
 };
 
 // words of workspace the two-level batch decoder needs

@@ -406,15 +406,17 @@ func (r *Reader) Close() {
 }
 
 // Reset restarts decoding from rd (reader.go:96-99).
-func (r *Reader) Reset(rd io.Reader) { r.ResetBytes(nil); r.Reader = rd }
+func (r *Reader) Reset(rd io.Reader) { r.ResetBytes(nil); r.Reader = rd; C.ez_reader_set_whole(r.h, 0) }
 
-// ResetBytes restarts decoding from b (reader.go:102-113).
+// ResetBytes restarts decoding from b (reader.go:102-113).  b is the whole stream: the handle
+// decodes it at once on the first Read and serves the Reads from that (ez_reader_set_whole).
 func (r *Reader) ResetBytes(b []byte) {
 	r.Reader = nil
 	r.b = b
 	r.i = 0
 	r.boff = 0
 	C.ez_reader_reset(r.h)
+	C.ez_reader_set_whole(r.h, 1)
 }
 
 // Read decompresses into p (reader.go:116-141).

@@ -151,6 +151,14 @@ int ez_reader_reset(ez_reader *r); /* the decoder part of ResetBytes reader.go:1
 int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size_t i, int64_t boff, uint8_t *p,
                    size_t p_len, size_t *n, size_t *i_out, int64_t *detail);
 int ez_reader_pending(const ez_reader *r); /* r.state != 0 (reader.go:135) */
+/* The b of this handle's Reads is the whole stream (NewReaderBytes / ResetBytes with no
+ * io.Reader behind it; no reference counterpart): the first Read of a fresh stream then decodes
+ * all of it at once on the device and the Reads are served from that output -- the same bytes,
+ * ErrBreak / errors / EOF at the same Reads (streams with a Break meta, an error, RequireMagic
+ * or SkipUnsupportedMeta keep the Read-by-Read decode). 0 (default): b may grow (NewReader). */
+int ez_reader_set_whole(ez_reader *r, int whole);
+/* 1 when this stream's Reads are being served from the whole-stream decode (tests, measurement). */
+int ez_reader_whole_decoded(const ez_reader *r);
 
 /* ---- device-resident batches of independent streams (the GPU hot path) ----
  * One stream = a fresh NewWriter(block, htable) receiving one Write; its

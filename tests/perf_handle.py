@@ -89,7 +89,29 @@ def main():
         t_r = time.perf_counter() - t0
         assert bytes(got) == b"".join(ws)
         res[str(size)]["reader_4k_MiBps"] = len(got) / t_r / 2**20
-    print(json.dumps({"handle_path": res, "writes_per_size": a.writes,
+    # Reader.Read(4 KiB) loop over a 16 MiB stream: NewReaderBytes (whole-stream decode on the first Read,
+    # ez_reader_set_whole) against the same handle decoding Read by Read (set_whole 0, NewReader's mode)
+    plain = src[: 16 << 20]
+    comp = orc.compress(1 << 20, 1024, [plain[k : k + 65536] for k in range(0, len(plain), 65536)])
+    rd = {}
+    for mode, whole in (("whole", 1), ("read_by_read", 0)):
+        r = ez.NewReaderBytes(comp)
+        L.ez_reader_set_whole(r._h, whole)
+        got = bytearray()
+        t0 = time.perf_counter()
+        while True:
+            d, err = r.Read(4096)
+            got += d
+            if err == ez.EOF:
+                break
+            assert err == ez.OK
+        t_r = time.perf_counter() - t0
+        assert bytes(got) == plain and r.whole_decoded == bool(whole)
+        rd[mode + "_MiBps"] = len(plain) / t_r / 2**20
+    t0 = time.perf_counter()
+    assert orc.decompress(comp, 4096)[0] == plain
+    rd["cpu_oracle_read4k_MiBps"] = len(plain) / (time.perf_counter() - t0) / 2**20
+    print(json.dumps({"handle_path": res, "writes_per_size": a.writes, "reader_16MiB_read4k": rd,
                       "note": "ez_writer_write per call: one pinned H2D copy, the general kernel (a wave), one D2H copy, one sync; "
                               "batch64: ez_writer_write_batch of 64 Writes per call"}))
 

@@ -518,3 +518,69 @@ def test_k2s_checks_and_forms(cuda):
                 assert torch.equal(out[s * cap : s * cap + n], ex[0][s * cap : s * cap + n]), (kind, cap, limit, s)
         if limit == 0:
             _cmp_oracle(ins, cap, res["s"][0].cpu().numpy(), res["s"][1].cpu().numpy(), res["s"][2].cpu().numpy())
+
+
+def test_reader_whole_decode_matches_read_by_read(cuda):
+    """NewReaderBytes decodes the whole stream on its first Read (ez_reader_set_whole) and serves
+    the Reads from it; with set_whole(0) (NewReader's mode) it decodes Read by Read.  Same bytes and the
+    same error sequence for a multi-block stream (Reset metas at every 1 MiB block), a stream with a
+    version header, one with a Break meta in the middle (decode-ahead declines: ErrBreak at the same
+    Read), a truncated stream and a corrupted one (both decline: the exact decoder's error)."""
+    import eazy_amd as ez
+    import impls
+    from eazy_amd import synth
+
+    G = impls.Gpu()
+    plain = synth.logs(91, 3 << 20).tobytes()
+    chunks = [plain[k : k + 200_000] for k in range(0, len(plain), 200_000)]
+
+    def stream(brk=False, hdr=False):
+        w = G.W(1 << 20, 1024)
+        if hdr:
+            w.append_magic = True
+            assert w.write_header() == ez.OK
+        for k, c in enumerate(chunks):
+            assert w.write(c) == (len(c), ez.OK)
+            if brk and k == len(chunks) // 2:
+                assert w.write_break() == ez.OK
+        return w.sink
+
+    def read_all(r, size):
+        out, errs = bytearray(), []
+        for _ in range(100_000):
+            got, err = r.read(size)
+            out += got
+            errs.append(err)
+            if err not in (ez.OK, ez.EBREAK):
+                break
+        return bytes(out), errs
+
+    clean = stream()
+    cases = {"clean": (clean, True), "header": (stream(hdr=True), True), "break": (stream(brk=True), False),
+             "truncated": (clean[: len(clean) - 7], False)}
+    bad = bytearray(clean)
+    bad[len(bad) // 2] ^= 0x5A
+    cases["corrupt"] = (bytes(bad), False)
+    for name, (comp, ahead) in cases.items():
+        for size in (4096, 1 << 20):
+            rb = G.Rb(comp)
+            got, errs = read_all(rb, size)
+            assert rb.r.whole_decoded == ahead, name
+            rx = G.Rb(comp)
+            ez._lib().ez_reader_set_whole(rx.r._h, 0)  # the same handle decoding Read by Read
+            want, werrs = read_all(rx, size)
+            assert not rx.r.whole_decoded
+            assert errs == werrs, (name, size, errs[-3:], werrs[-3:])
+            assert got == want, (name, size)
+            if name in ("clean", "header", "break"):
+                assert got == plain and errs[-1] == ez.EOF, name
+            if name == "break":
+                assert errs.count(ez.EBREAK) == 1
+    # ResetBytes starts a new whole decode; Reset(io.Reader) goes back to Read by Read
+    rb = G.Rb(clean)
+    assert rb.read(10)[0] == plain[:10] and rb.r.whole_decoded
+    rb.reset_bytes(clean)
+    assert not rb.r.whole_decoded
+    assert rb.read(1 << 22)[0] == plain and rb.r.whole_decoded
+    rb.reset(clean)
+    assert read_all(rb, 1 << 16)[0] == plain and not rb.r.whole_decoded
