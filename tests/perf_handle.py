@@ -99,8 +99,10 @@ def main():
         L.ez_reader_set_whole(r._h, whole)
         got = bytearray()
         t0 = time.perf_counter()
+        t1 = None
         while True:
             d, err = r.Read(4096)
+            t1 = t1 or time.perf_counter()
             got += d
             if err == ez.EOF:
                 break
@@ -108,6 +110,7 @@ def main():
         t_r = time.perf_counter() - t0
         assert bytes(got) == plain and r.whole_decoded == bool(whole)
         rd[mode + "_MiBps"] = len(plain) / t_r / 2**20
+        rd[mode + "_first_read_ms"] = (t1 - t0) * 1e3
     t0 = time.perf_counter()
     assert orc.decompress(comp, 4096)[0] == plain
     rd["cpu_oracle_read4k_MiBps"] = len(plain) / (time.perf_counter() - t0) / 2**20
