@@ -92,7 +92,7 @@ def _enc(fn, a, b):
     e = getattr(lib(), fn)(buf, C.byref(n), a, b)
     if e == EINVAL:
         raise Panic(fn)
-    return bytes(buf[: n.value])
+    return C.string_at(buf, n.value)
 
 
 def enc_tag(tag, l):
@@ -211,7 +211,7 @@ class Reader:
         buf = (C.c_uint8 * max(n, 1))()
         got = _i64()
         e = lib().or_reader_read(self._r, buf, n, C.byref(got))
-        return bytes(buf[: got.value]), e
+        return C.string_at(buf, got.value), e
 
     def reset_bytes(self, b: bytes):
         lib().or_reader_reset_bytes(self._r, bytes(b), len(b))
@@ -230,7 +230,7 @@ def compress(block, htable, writes, append_magic=True, ver=0) -> bytes:
     e = lib().or_compress(block, htable, int(append_magic), ver, data, lens, len(writes), out, cap, C.byref(n))
     if e:
         raise RuntimeError(f"or_compress: {e}")
-    return bytes(out[: n.value])
+    return C.string_at(out, n.value)
 
 
 def decompress(b: bytes, buf_size: int = 1 << 16, cap: int | None = None):
@@ -238,7 +238,7 @@ def decompress(b: bytes, buf_size: int = 1 << 16, cap: int | None = None):
     out = (C.c_uint8 * cap)()
     n, nb = _i64(), _i64()
     e = lib().or_decompress(bytes(b), len(b), buf_size, out, cap, C.byref(n), C.byref(nb))
-    return bytes(out[: n.value]), e, nb.value
+    return C.string_at(out, n.value), e, nb.value
 
 
 def _ptr(a: np.ndarray):
