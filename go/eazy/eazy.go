@@ -406,7 +406,12 @@ func (r *Reader) Close() {
 }
 
 // Reset restarts decoding from rd (reader.go:96-99).
-func (r *Reader) Reset(rd io.Reader) { r.ResetBytes(nil); r.Reader = rd; C.ez_reader_set_whole(r.h, 0) }
+func (r *Reader) Reset(rd io.Reader) {
+	r.ResetBytes(nil)
+	r.Reader = rd
+	C.ez_reader_set_whole(r.h, 0)
+	runtime.KeepAlive(r)
+}
 
 // ResetBytes restarts decoding from b (reader.go:102-113).  b is the whole stream: the handle
 // decodes it at once on the first Read and serves the Reads from that (ez_reader_set_whole).
@@ -417,6 +422,7 @@ func (r *Reader) ResetBytes(b []byte) {
 	r.boff = 0
 	C.ez_reader_reset(r.h)
 	C.ez_reader_set_whole(r.h, 1)
+	runtime.KeepAlive(r)
 }
 
 // Read decompresses into p (reader.go:116-141).

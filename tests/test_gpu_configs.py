@@ -356,6 +356,51 @@ def test_k2t_copy_chains_within_rounds(cuda):
             assert got[offs[s] : offs[s + 1]] == b, f"K2 {kind!r}: stream {s} (len {lens[s]}) differs"
 
 
+def _defer_stream(rng, n_lit):
+    """A literal long enough for K2t/K2w to defer (>= 16 KiB of random bytes), then what reads
+    it back: a short-period run seeded by its last bytes, copies from its tail and its middle, and
+    more of the same after some fresh bytes."""
+    lit = rng.integers(0, 256, n_lit, dtype=np.uint8).tobytes()
+    per = int(rng.integers(1, 16))
+    out = lit + lit[-per:] * int(rng.integers(3, 40))
+    out += lit[-200:-100] + lit[n_lit // 2 : n_lit // 2 + 300]
+    out += rng.integers(0, 256, 50, dtype=np.uint8).tobytes() + lit[-24:] + lit[100:140]
+    return out
+
+
+@pytest.mark.gpu
+def test_k2t_deferred_literal_neighbours(cuda):
+    """K2t does not put a deferred literal (>= 16 KiB, moved later by kd_copy) into its ring: the
+    copies and runs that read it right after take its bytes from the input.  Streams of a long
+    literal followed by such readers, decoded in a small batch (the 32/64 KiB-ring K2t) and inside
+    a batch of 1,100 streams (4/8 KiB rings), every K2 decoder against the input."""
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(97)
+    defer = [_defer_stream(rng, int(n)) for n in rng.integers(16384, 90000, 12)]
+    filler = [synth.logs(300 + k, 6000).tobytes() for k in range(1100 - len(defer))]
+    for bufs in (defer, defer + filler):
+        want = [orc.compress(MiB, 1024, [b]) for b in bufs]
+        lens = [len(b) for b in bufs]
+        coff = np.concatenate([[0], np.cumsum([len(w) for w in want])]).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+        comp = torch.from_numpy(np.frombuffer(b"".join(want) + bytes(64), np.uint8).copy()).to(cuda)
+        d_coff, d_offs = torch.from_numpy(coff).to(cuda), torch.from_numpy(offs).to(cuda)
+        for kind in ("t", "w", ""):
+            ez.select_decompress_kernel(kind)
+            try:
+                out, sz, st = ez.decompress_batch(comp, d_coff, d_offs)
+            finally:
+                ez.select_decompress_kernel("")
+            assert st.abs().sum().item() == 0, kind
+            got = out[: int(offs[-1])].cpu().numpy().tobytes()
+            for s, b in enumerate(bufs):
+                assert got[offs[s] : offs[s + 1]] == b, f"K2 {kind!r}: stream {s} (len {lens[s]}) of {len(bufs)} differs"
+
+
 @pytest.mark.gpu
 def test_decoder_routing_without_hint(cuda):
     """The batch decoder follows the largest output slot, measured on the device when the
