@@ -522,24 +522,31 @@ struct WinRoll {
         bmax = floor4(n - 64);
         cb = min(floor4(-8), bmax);
         fb = min(cb + 64, bmax);
-        c0 = c1 = f0 = f1 = 0;
-        if (live) {
-            ld(p, cb, lj, c0, c1);
-            ld(p, fb, lj, f0, f1);
-        }
+        f0 = f1 = 0;
+        if (live) ld(p, cb, lj, f0, f1);
+        // (c only ever from these moves: no load is pending on c's registers at the loop's head, where
+        // a wait for one would wait for the prefetch behind it too)
+        asm volatile("v_mov_b32 %0, %1" : "=v"(c0) : "v"(f0));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(c1) : "v"(f1));
+        if (live) ld(p, fb, lj, f0, f1);
     }
     // the region for the window at i (group-uniform), after this window's gathers
+    // (one path for both cases -- the region moves from f to c, the next one is loaded into f -- so
+    // that the prefetch lands in f's registers: with the long jump loading c in a branch of its own,
+    // the merged c took f's registers, the prefetch went to others and was copied into f's at once,
+    // a wait for the load just issued on every region switch)
     __device__ __forceinline__ void advance(const uint8_t *p, int32_t i, int lj, bool live) {
         const int32_t y = i - 8;
         if (live && !(y >= cb && y - cb <= 80)) {
-            if (y >= fb && y - fb <= 80) {
-                cb = fb;
-                c0 = f0;
-                c1 = f1;
-            } else {  // a long jump: the region is loaded on the chain
-                cb = min(floor4(y), bmax);
-                ld(p, cb, lj, c0, c1);
+            if (!(y >= fb && y - fb <= 80)) {  // a long jump: the region is loaded on the chain
+                fb = min(floor4(y), bmax);
+                ld(p, fb, lj, f0, f1);
             }
+            cb = fb;
+            // (moves the compiler cannot sink past the load below: phi copies placed after it made
+            // it load f elsewhere and copy at once)
+            asm volatile("v_mov_b32 %0, %1" : "=v"(c0) : "v"(f0));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(c1) : "v"(f1));
             fb = min(cb + 64, bmax);
             ld(p, fb, lj, f0, f1);
         }
@@ -839,15 +846,13 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
                 if (TB == 12) lds_put12((uint64_t *)hth, h1, (uint32_t)(x + 1));
                 else hth[h1] = (uint16_t)(x + 1);
             }
-#if !(EZ_EXP & 32768)
-            if ((uint64_t)nrec < rcap) {
-                if (NT) __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), recw + (roff + (uint32_t)nrec));
-                else recw[roff + (uint32_t)nrec] = rec_pack(lit, nx - lit, dist, force);
-            }
-#else  // (timing builds: the records' traffic without their lines -- k1_emit then sees none)
-            __builtin_nontemporal_store(rec_pack(lit, nx - lit, dist, force), recw + (roff + (uint32_t)(nrec & 1)));
-#endif
         }
+        // the record, stored after the next region's load is issued (a region switch waits for every
+        // vector-memory operation before it, stores included)
+        const bool st_rec = act && lj == a;
+        const uint64_t rec = rec_pack(lit, nx - lit, dist, force);
+        const uint32_t rat = roff + (uint32_t)nrec;
+        const bool rec_room = (uint64_t)nrec < rcap;
         if (act) {
             if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
             nrec++;
@@ -857,6 +862,17 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         }
         if (live && (err || i + 4 > n)) live = false;
         wr.advance(p, i, lj, live);  // the next window's region
+        __builtin_amdgcn_sched_barrier(0);
+        if (st_rec) {
+#if !(EZ_EXP & 32768)
+            if (rec_room) {
+                if (NT) __builtin_nontemporal_store(rec, recw + rat);
+                else recw[rat] = rec;
+            }
+#else  // (timing builds: the records' traffic without their lines -- k1_emit then sees none)
+            __builtin_nontemporal_store(rec, recw + (roff + (uint32_t)(nrec & 1)));
+#endif
+        }
     }
     nrec_out = nrec;
 }
@@ -901,28 +917,29 @@ struct WinRollL {
             d1 = dw_chk(a + 4, lo, hi);
         }
     }
+    // (as WinRoll: c only from moves after f's load, so the prefetch lands in f's registers and no wait
+    // for it is put at the loop's head)
     __device__ __forceinline__ void init(const uint8_t *p, int32_t i, int lj, bool live, const uint8_t *lo, const uint8_t *hi) {
         pm = (int32_t)((uintptr_t)p & 3);
         cb = floor4(i - 8);
         fb = cb + 64;
-        c0 = c1 = f0 = f1 = 0;
-        if (live) {
-            ld(p, cb, lj, lo, hi, c0, c1);
-            ld(p, fb, lj, lo, hi, f0, f1);
-        }
+        f0 = f1 = 0;
+        if (live) ld(p, cb, lj, lo, hi, f0, f1);
+        asm volatile("v_mov_b32 %0, %1" : "=v"(c0) : "v"(f0));
+        asm volatile("v_mov_b32 %0, %1" : "=v"(c1) : "v"(f1));
+        if (live) ld(p, fb, lj, lo, hi, f0, f1);
     }
     // the region for the window at i (group-uniform: 0 <= i - 8 - cb <= 64), after this window's gathers
     __device__ __forceinline__ void advance(const uint8_t *p, int32_t i, int lj, bool live, const uint8_t *lo, const uint8_t *hi) {
         const int32_t y = i - 8;
         if (live && !(y >= cb && y - cb <= 64)) {
-            if (y >= fb && y - fb <= 64) {
-                cb = fb;
-                c0 = f0;
-                c1 = f1;
-            } else {  // a long jump (or back: the cut branch): the region is loaded on the chain
-                cb = floor4(y);
-                ld(p, cb, lj, lo, hi, c0, c1);
+            if (!(y >= fb && y - fb <= 64)) {  // a long jump (or back: the cut branch): loaded on the chain
+                fb = floor4(y);
+                ld(p, fb, lj, lo, hi, f0, f1);
             }
+            cb = fb;
+            asm volatile("v_mov_b32 %0, %1" : "=v"(c0) : "v"(f0));
+            asm volatile("v_mov_b32 %0, %1" : "=v"(c1) : "v"(f1));
             fb = cb + 64;
             ld(p, fb, lj, lo, hi, f0, f1);
         }
@@ -1282,9 +1299,11 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
         if (valid && (a < 0 || lj <= a)) htw[h] = (uint32_t)x;
         if (act && lj == a) {
             if (!rl && !zr && x + 1 + 4 <= n) htw[((uint32_t)(w0.hi >> 8) * kHashMul) >> hsh] = (uint32_t)(x + 1);
-            if ((uint64_t)nrec < rcap)
-                __builtin_nontemporal_store(u32x4{(uint32_t)lit, (uint32_t)(nx - lit), (uint32_t)dist, force ? 1u : 0u}, (u32x4 *)(rec + nrec));
         }
+        // the record, stored after the next region's load is issued (as in lean_loop)
+        const bool st_rec = act && lj == a && (uint64_t)nrec < rcap;
+        const u32x4 recv{(uint32_t)lit, (uint32_t)(nx - lit), (uint32_t)dist, force ? 1u : 0u};
+        u32x4 *const recp = (u32x4 *)(rec + nrec);
         if (act) {
             if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
             nrec++;
@@ -1294,6 +1313,8 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
         }
         if (live && (err || i + 4 > n)) live = false;
         if (!kWinSrc) wr.advance(p, i, lj, live, blo, bhi);  // the next window's region
+        __builtin_amdgcn_sched_barrier(0);
+        if (st_rec) __builtin_nontemporal_store(recv, recp);
         EZ_PROF_MARK(5);
     }
 #if (EZ_EXP & 4)

@@ -130,6 +130,13 @@ __device__ __forceinline__ void rput_fast(uint8_t *ring, int32_t p, V16 v, uint3
     }
 }
 
+// the 16 bytes from x: the first k (0..16) from a, the rest from b
+__device__ __forceinline__ V16 merge16(V16 a, V16 b, int32_t k) {
+    const uint32_t kl = (uint32_t)(k < 8 ? k : 8), kh = (uint32_t)(k < 8 ? 0 : k - 8);
+    const uint64_t ml = kl >= 8 ? ~0ull : (1ull << (8 * kl)) - 1, mh = kh >= 8 ? ~0ull : (1ull << (8 * kh)) - 1;
+    return V16{(a.lo & ml) | (b.lo & ~ml), (a.hi & mh) | (b.hi & ~mh)};
+}
+
 // bytes a run of period per (1..15) advances per 16-byte pattern store
 __device__ __forceinline__ int32_t run_step_of(int32_t per) { return per * (16 / per); }
 
@@ -177,44 +184,16 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
     if (in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16) HANDOVER(1);
     const int32_t nb = (int32_t)nb64, cap = (int32_t)cap64;
 
-    // the next window's input, loaded while this one is decoded: [pb, pb + kTWin + 16 * kPfX) with pb =
-    // this window's base + kTWin (the next base is the chain's entry rounded down: usually pb or a
-    // piece or two past it); lane k holds pieces k and kTWin / 16 + k (k < kPfX)
-    constexpr int32_t kPfX = 10;
-    V16 pf0{0, 0}, pf1{0, 0};
-    int32_t pb = -1;
     while (w < nb) {
         const int32_t base = w & ~15;
-        // ---- stage the window [base, base + kTStage) (bytes past the batch read 0): from the
-        // prefetched pieces when they cover it, else loaded now
-        const int32_t sh = base - pb;
-        if (pb >= 0 && sh >= 0 && sh + kTStage <= kTWin + 16 * kPfX) {
-            const int32_t k0 = 16 * lane - sh, k1 = kTWin + 16 * lane - sh;
-            if (k0 >= 0) {
-                *(u64_ua *)(inb + k0) = pf0.lo;
-                *(u64_ua *)(inb + k0 + 8) = pf0.hi;
-            }
-            if (lane < kPfX && k1 < kTStage) {
-                *(u64_ua *)(inb + k1) = pf1.lo;
-                *(u64_ua *)(inb + k1 + 8) = pf1.hi;
-            }
-        } else {
-            for (int32_t k = 16 * lane; k < kTStage; k += 16 * kWave) {
-                const uint8_t *y = b + base + k;
-                const V16 v = y + 16 <= in_end ? ld16v(y) : ld_clamped(y, A.in, in_end);
-                *(u64_ua *)(inb + k) = v.lo;
-                *(u64_ua *)(inb + k + 8) = v.hi;
-            }
+        // ---- stage the window [base, base + kTStage) (bytes past the batch read 0)
+        for (int32_t k = 16 * lane; k < kTStage; k += 16 * kWave) {
+            const uint8_t *y = b + base + k;
+            const V16 v = y + 16 <= in_end ? ld16v(y) : ld_clamped(y, A.in, in_end);
+            *(u64_ua *)(inb + k) = v.lo;
+            *(u64_ua *)(inb + k + 8) = v.hi;
         }
         __syncthreads();
-        pb = base + kTWin;
-        if (pb < nb) {  // (uniform)
-            const uint8_t *y0 = b + pb + 16 * lane, *y1 = b + pb + kTWin + 16 * lane;
-            pf0 = y0 + 16 <= in_end ? ld16v(y0) : ld_clamped(y0, A.in, in_end);
-            if (lane < kPfX) pf1 = y1 + 16 <= in_end ? ld16v(y1) : ld_clamped(y1, A.in, in_end);
-        } else {
-            pb = -1;
-        }
         // ---- scan: the advance of every position base + 16 * lane + j (lane's segment)
         uint32_t ad[4];
         {
@@ -556,7 +535,10 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                     V16 pv{0, 0};
                     int32_t stp = 16;
                     if (slow && D > 0 && D < 16) {
-                        const V16 v = dst - 16 >= rv ? zero_before_start(rld<R>(ring, dst - 16), dst - 16) : far16(out, cap, b, dst - 16, nd, defs);
+                        // (the bytes before rv, a deferred literal's, are not in the ring: from the input;
+                        // those after it are, and are not in HBM yet)
+                        V16 v = zero_before_start(rld<R>(ring, dst - 16), dst - 16);
+                        if (dst - 16 < rv) v = merge16(far16(out, cap, b, dst - 16, nd, defs), v, rv - (dst - 16));
                         pv = run_pattern(shr16(v, (uint32_t)(16 - D)), (uint32_t)D);
                         stp = run_step_of(D);
                     }
@@ -566,8 +548,13 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                             V16 v = pv;  // a run's pattern; a zero region's zeros
                             if (D >= 16) {
                                 const int32_t x = ys + o;
-                                if (x >= ringlo) v = zero_before_start(rld<R>(ring, x), x);
-                                else v = far16(out, cap, b, x, nd, defs);  // flushed already (or deferred)
+                                if (x >= ringlo) {
+                                    v = zero_before_start(rld<R>(ring, x), x);
+                                } else {
+                                    v = far16(out, cap, b, x, nd, defs);  // flushed already (or deferred)
+                                    // past a deferred literal's end the bytes are in the ring, not in HBM
+                                    if (x + 16 > rv && x < rv) v = merge16(v, rld<R>(ring, x), rv - x);
+                                }
                             }
                             rput<R>(ring, dst + o, v, (uint32_t)(L - o < 16 ? L - o : 16));
                         }
