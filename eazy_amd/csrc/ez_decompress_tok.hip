@@ -64,8 +64,7 @@ struct TLayout {
     // a source farther back than the ring is already in HBM (unflushed output stays < 1 KiB)
     static constexpr int32_t budget = R - 1024 - 64;
     static_assert(budget >= kTBig, "a round must hold any token that is not moved alone");
-    // literals of kDeferMin bytes or more go to kd_copy; the ring does not hold them (rv below)
-    static constexpr int32_t defer_min = kDeferMin;
+    static_assert(kDeferMin > R, "a deferred literal refills the whole ring");
 };
 
 __device__ __forceinline__ uint32_t fanout(uint32_t f) { return f | (f - (f >> 7)); }  // bit 7 of a byte -> 0xff
@@ -130,13 +129,6 @@ __device__ __forceinline__ void rput_fast(uint8_t *ring, int32_t p, V16 v, uint3
     }
 }
 
-// the 16 bytes from x: the first k (0..16) from a, the rest from b
-__device__ __forceinline__ V16 merge16(V16 a, V16 b, int32_t k) {
-    const uint32_t kl = (uint32_t)(k < 8 ? k : 8), kh = (uint32_t)(k < 8 ? 0 : k - 8);
-    const uint64_t ml = kl >= 8 ? ~0ull : (1ull << (8 * kl)) - 1, mh = kh >= 8 ? ~0ull : (1ull << (8 * kh)) - 1;
-    return V16{(a.lo & ml) | (b.lo & ~ml), (a.hi & mh) | (b.hi & ~mh)};
-}
-
 // bytes a run of period per (1..15) advances per 16-byte pattern store
 __device__ __forceinline__ int32_t run_step_of(int32_t per) { return per * (16 / per); }
 
@@ -180,7 +172,6 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
     const int64_t limit = A.block_size_limit;
     const int32_t lim32 = limit == 0 || limit > 0x7fffffff ? 0x7fffffff : (int32_t)limit;
     int32_t w = 0, pos = 0, fl = 0, bsl = -1;  // w: the chain's entry into the next window; fl: output below is in HBM
-    int32_t rv = -0x40000000;  // the ring holds no output below rv (the end of the last deferred literal)
     if (in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16) HANDOVER(1);
     const int32_t nb = (int32_t)nb64, cap = (int32_t)cap64;
 
@@ -374,9 +365,9 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                     else put_small(out + x, v, (uint32_t)(pos - x));
                 }
                 __builtin_amdgcn_s_waitcnt(0);  // (stores done before the copy reads them back)
-                if (!cp0 && L0 >= Lay::defer_min && nd < kDefSlots && A.defer) {
+                if (!cp0 && L0 >= kDeferMin && nd < kDefSlots && A.defer) {
                     // a long literal: recorded for kd_copy (the chip moves it after the decoders); the
-                    // ring does not get its bytes (copies reading them take them from the input, far16)
+                    // ring gets its last bytes from the input
                     if (lane == 0) {
                         const uint32_t at = atomicAdd(&A.defer[0], 1u);
                         if (at < A.defer_cap)
@@ -386,8 +377,11 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                         defs[3 * nd + 2] = L0;
                     }
                     nd++;
+                    for (int32_t x = L0 - R + 16 * lane; x < L0; x += 16 * kWave) {  // (L0 > R)
+                        const uint8_t *y = b + src0 + x;
+                        rput<R>(ring, pos + x, y + 16 <= in_end ? ld16v(y) : ld_clamped(y, A.in, in_end), (uint32_t)(L0 - x < 16 ? L0 - x : 16));
+                    }
                     pos += L0;
-                    rv = pos;
                     fl = pos;
                     t0 += 1;
                     __syncthreads();
@@ -412,7 +406,7 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                         __builtin_amdgcn_s_waitcnt(0);
                     }
                 } else {  // a short-period run: its 16-byte pattern every step bytes
-                    V16 v = pos - 16 >= rv ? zero_before_start(rld<R>(ring, pos - 16), pos - 16) : far16(out, cap, b, pos - 16, nd, defs);
+                    V16 v = zero_before_start(rld<R>(ring, pos - 16), pos - 16);
                     const V16 pv = run_pattern(shr16(v, (uint32_t)(16 - D0)), (uint32_t)D0);
                     const int32_t stp = run_step_of(D0);
                     for (int32_t k = stp * lane; k < L0; k += stp * kWave) {
@@ -460,7 +454,7 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
             const int32_t D = (int32_t)tk.D;
             const int32_t cs = dst - D;
             const int32_t need = D == 0 ? -0x7fffffff : cs + (D < L ? D : L);
-            const int32_t ringlo = max(pos + total - R + 16, rv);  // sources from here on are in the ring
+            const int32_t ringlo = pos + total - R + 16;  // sources from here on are in the ring
             uint64_t cm = (EZ_EXP & 256) ? 0 : __ballot(cpy);
             // ---- sources final at the round's start (every copy marked fre may run in any batch):
             // zero regions, sources before the round, sources inside one literal of the round (all
@@ -535,10 +529,7 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                     V16 pv{0, 0};
                     int32_t stp = 16;
                     if (slow && D > 0 && D < 16) {
-                        // (the bytes before rv, a deferred literal's, are not in the ring: from the input;
-                        // those after it are, and are not in HBM yet)
-                        V16 v = zero_before_start(rld<R>(ring, dst - 16), dst - 16);
-                        if (dst - 16 < rv) v = merge16(far16(out, cap, b, dst - 16, nd, defs), v, rv - (dst - 16));
+                        const V16 v = zero_before_start(rld<R>(ring, dst - 16), dst - 16);
                         pv = run_pattern(shr16(v, (uint32_t)(16 - D)), (uint32_t)D);
                         stp = run_step_of(D);
                     }
@@ -548,13 +539,8 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                             V16 v = pv;  // a run's pattern; a zero region's zeros
                             if (D >= 16) {
                                 const int32_t x = ys + o;
-                                if (x >= ringlo) {
-                                    v = zero_before_start(rld<R>(ring, x), x);
-                                } else {
-                                    v = far16(out, cap, b, x, nd, defs);  // flushed already (or deferred)
-                                    // past a deferred literal's end the bytes are in the ring, not in HBM
-                                    if (x + 16 > rv && x < rv) v = merge16(v, rld<R>(ring, x), rv - x);
-                                }
+                                if (x >= ringlo) v = zero_before_start(rld<R>(ring, x), x);
+                                else v = far16(out, cap, b, x, nd, defs);  // flushed already (or deferred)
                             }
                             rput<R>(ring, dst + o, v, (uint32_t)(L - o < 16 ? L - o : 16));
                         }
@@ -607,11 +593,6 @@ __global__ __launch_bounds__(64) void k2_tok(DecompressArgs A) {
 // rounds of resident waves, the last one partly empty, so R = 4096 is taken whenever it needs
 // fewer such rounds (C2, 4,096 x 256 KiB: 3,072 resident waves at 8 KiB, all 4,096 at 4 KiB:
 // K2 7.06 -> 4.93 ms), and always when the whole stream fits it.
-// Batches that fit the chip at 32 or 64 KiB per wave in one round (<= 1,024 / <= 512 streams:
-// 1 MiB streams, C4's buckets, a Reader handle's whole-stream decode) take that ring: a copy whose
-// source lies past the ring reads HBM after the flush stores have drained (`s_waitcnt` 0), ~2 us
-// of a lone wave's chain, and on log streams 2.6 % of the copies reach past 7 KiB (about one per
-// 64-token round) but 0.3 % past 16 KiB and none past 63 KiB.
 static uint64_t resident_waves(const void *kernel, size_t lds) {
     int dev = 0, ncu = 0, per = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
@@ -621,24 +602,12 @@ static uint64_t resident_waves(const void *kernel, size_t lds) {
 }
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t st) {
     const uint64_t grid = a.count < (1u << 30) ? a.count : (1u << 30);
-    static const int force_r = knob("EZ_K2T_R", 0);  // A/B (experiment builds): 4096 / 8192 / 32768 / 65536
-    static const bool attr = [] {
-        (void)hipFuncSetAttribute((const void *)k2_tok<32768>, hipFuncAttributeMaxDynamicSharedMemorySize, TLayout<32768>::bytes);
-        (void)hipFuncSetAttribute((const void *)k2_tok<65536>, hipFuncAttributeMaxDynamicSharedMemorySize, TLayout<65536>::bytes);
-        return true;
-    }();
-    (void)attr;
+    static const int force_r = knob("EZ_K2T_R", 0);  // A/B (experiment builds): 4096 / 8192
     static const uint64_t res4 = resident_waves((const void *)k2_tok<4096>, TLayout<4096>::bytes);
     static const uint64_t res8 = resident_waves((const void *)k2_tok<8192>, TLayout<8192>::bytes);
-    static const uint64_t res32 = resident_waves((const void *)k2_tok<32768>, TLayout<32768>::bytes);
-    static const uint64_t res64 = resident_waves((const void *)k2_tok<65536>, TLayout<65536>::bytes);
     const bool fits = a.max_out != 0 && a.max_out <= 4096;  // the whole stream fits the ring
     const bool fewer_rounds = (grid + res4 - 1) / res4 < (grid + res8 - 1) / res8;
-    if (force_r == 65536 || (force_r == 0 && !fits && grid <= res64)) {
-        hipLaunchKernelGGL(k2_tok<65536>, dim3((unsigned)grid), dim3(64), TLayout<65536>::bytes, st, a);
-    } else if (force_r == 32768 || (force_r == 0 && !fits && grid <= res32)) {
-        hipLaunchKernelGGL(k2_tok<32768>, dim3((unsigned)grid), dim3(64), TLayout<32768>::bytes, st, a);
-    } else if (force_r == 4096 || (force_r == 0 && (fits || fewer_rounds))) {
+    if (force_r == 4096 || (force_r == 0 && (fits || fewer_rounds))) {
         hipLaunchKernelGGL(k2_tok<4096>, dim3((unsigned)grid), dim3(64), TLayout<4096>::bytes, st, a);
     } else {
         hipLaunchKernelGGL(k2_tok<8192>, dim3((unsigned)grid), dim3(64), TLayout<8192>::bytes, st, a);
