@@ -575,6 +575,64 @@ struct WinRoll {
     }
 };
 
+// WinRoll with the current region in LDS (LW, experiments): the group's 144-byte buffer holds stream
+// bytes [cb, cb + 128); a window's 32 bytes are nine aligned dword reads and eight v_alignbyte, instead
+// of ten ds_bpermute, nine selects and eight v_alignbyte from the lanes' registers
+struct WinLds {
+    uint32_t f0, f1;  // this lane's dwords of the prefetched region
+    int32_t cb, fb, bmax, pm;
+    uint8_t *wl;  // the group's buffer (LDS)
+    __device__ __forceinline__ int32_t floor4(int32_t y) const { return y - ((pm + y) & 3); }
+    __device__ __forceinline__ void ld(const uint8_t *p, int32_t b, int lj, uint32_t &d0, uint32_t &d1) const {
+        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+        typedef const __attribute__((address_space(1))) u32x2 *gu64p;
+        const u32x2 v = *(gu64p)(p + b + 8 * lj);
+        d0 = v.x;
+        d1 = v.y;
+    }
+    __device__ __forceinline__ void put(int lj) const {
+        *(uint64_t *)(wl + 8 * lj) = (uint64_t)f0 | ((uint64_t)f1 << 32);
+    }
+    __device__ __forceinline__ void init(const uint8_t *p, int32_t n, int lj, bool live) {
+        pm = (int32_t)((uintptr_t)p & 3);
+        bmax = floor4(n - 64);
+        cb = min(floor4(-8), bmax);
+        fb = min(cb + 64, bmax);
+        f0 = f1 = 0;
+        if (live) ld(p, cb, lj, f0, f1);
+        put(lj);
+        if (live) ld(p, fb, lj, f0, f1);
+    }
+    __device__ __forceinline__ void advance(const uint8_t *p, int32_t i, int lj, bool live) {
+        const int32_t y = i - 8;
+        if (live && !(y >= cb && y - cb <= 80)) {
+            if (!(y >= fb && y - fb <= 80)) {
+                fb = min(floor4(y), bmax);
+                ld(p, fb, lj, f0, f1);
+            }
+            cb = fb;
+            put(lj);
+            fb = min(cb + 64, bmax);
+            ld(p, fb, lj, f0, f1);
+        }
+    }
+    __device__ __forceinline__ void bytes(int32_t i, int g, int lj, V16 &w0, V16 &w1) const {
+        const uint32_t o = (uint32_t)(i - 8 - cb + lj), r = o & 3;
+        const uint32_t *q = (const uint32_t *)(wl + (o & ~3u));
+        uint32_t d[9];
+#pragma unroll
+        for (int t = 0; t < 9; t++) d[t] = q[t];
+        uint32_t b[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+        w0.lo = (uint64_t)b[0] | ((uint64_t)b[1] << 32);
+        w0.hi = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
+        w1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
+        w1.hi = (uint64_t)b[6] | ((uint64_t)b[7] << 32);
+    }
+};
+constexpr int32_t kWinLdsBytes = 144;
+
 // The 32 bytes y-8 .. y+23 by dword-aligned loads (dwordx4, dwordx4, dword from floor4(p + y - 8))
 // and v_alignbyte: a 16-byte load at a byte-unaligned address costs the L1 one access per dword it
 // touches, an aligned one a single access (tools/mb_ta.hip, L1-resident: 64 vs 16 ns per scattered
@@ -715,17 +773,18 @@ __device__ __forceinline__ void lds_put12(uint64_t *tab, uint32_t h, uint32_t va
 
 // TB: the table's visit -- 0 the DPP search over a u16 table, 16 lds_mskor16, 12 lds_mskor12;
 // NT: the records are stored nontemporal (read back by another kernel) or plain (by this wave)
-template <int TB, bool NT = true>
+template <int TB, bool NT = true, bool LW = false>
 __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int32_t n, int lj, int g, uint16_t *hth,
                                           uint32_t hsh, uint64_t *recw, uint32_t roff, uint64_t rcap, int prio, int32_t &nrec_out,
-                                          int &err) {
+                                          int &err, uint8_t *wl = nullptr) {
     // (the records at recw + roff: recw is the wave's, in scalar registers, roff the group's)
     constexpr int G = 16;
     int32_t i = 0, done = 0, nrec = 0;
     bool live = !err && n >= 4;
     int32_t guard = 4 * n + 64;
     V16 w0{0, 0}, w1{0, 0};  // bytes x-8 .. x+7 and x+8 .. x+23 of this lane's position x
-    WinRoll wr;
+    typename std::conditional<LW, WinLds, WinRoll>::type wr;
+    if constexpr (LW) wr.wl = wl;
     wr.init(p, n, lj, live);
     // the bytes around stream position 0, the candidate of every zero table entry:
     // judged without a load
@@ -965,6 +1024,50 @@ struct WinRollL {
         w2 = V16{(uint64_t)b[8] | ((uint64_t)b[9] << 32), (uint64_t)b[10] | ((uint64_t)b[11] << 32)};
     }
 };
+// WinRollL with the current region in LDS (as WinLds): the group's buffer holds stream bytes
+// [cb, cb + 128); a window's 48 bytes are thirteen aligned dword reads and twelve v_alignbyte
+struct WinLdsL {
+    uint32_t f0, f1;  // this lane's dwords of the prefetched region
+    int32_t cb, fb, pm;
+    uint8_t *wl;  // the group's buffer (LDS)
+    __device__ __forceinline__ int32_t floor4(int32_t y) const { return y - ((pm + y) & 3); }
+    __device__ __forceinline__ void put(int lj) const { *(uint64_t *)(wl + 8 * lj) = (uint64_t)f0 | ((uint64_t)f1 << 32); }
+    __device__ __forceinline__ void init(const uint8_t *p, int32_t i, int lj, bool live, const uint8_t *lo, const uint8_t *hi) {
+        pm = (int32_t)((uintptr_t)p & 3);
+        cb = floor4(i - 8);
+        fb = cb + 64;
+        f0 = f1 = 0;
+        if (live) WinRollL::ld(p, cb, lj, lo, hi, f0, f1);
+        put(lj);
+        if (live) WinRollL::ld(p, fb, lj, lo, hi, f0, f1);
+    }
+    __device__ __forceinline__ void advance(const uint8_t *p, int32_t i, int lj, bool live, const uint8_t *lo, const uint8_t *hi) {
+        const int32_t y = i - 8;
+        if (live && !(y >= cb && y - cb <= 64)) {
+            if (!(y >= fb && y - fb <= 64)) {  // a long jump (or back: the cut branch): loaded on the chain
+                fb = floor4(y);
+                WinRollL::ld(p, fb, lj, lo, hi, f0, f1);
+            }
+            cb = fb;
+            put(lj);
+            fb = cb + 64;
+            WinRollL::ld(p, fb, lj, lo, hi, f0, f1);
+        }
+    }
+    __device__ __forceinline__ void bytes48(int32_t i, int g, int lj, V16 &w0, V16 &w1, V16 &w2) const {
+        const uint32_t o = (uint32_t)(i - 8 - cb + lj), r = o & 3;  // o <= 79
+        const uint32_t *q = (const uint32_t *)(wl + (o & ~3u));
+        uint32_t d[13];
+#pragma unroll
+        for (int t = 0; t < 13; t++) d[t] = q[t];
+        uint32_t b[12];
+#pragma unroll
+        for (int t = 0; t < 12; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+        w0 = V16{(uint64_t)b[0] | ((uint64_t)b[1] << 32), (uint64_t)b[2] | ((uint64_t)b[3] << 32)};
+        w1 = V16{(uint64_t)b[4] | ((uint64_t)b[5] << 32), (uint64_t)b[6] | ((uint64_t)b[7] << 32)};
+        w2 = V16{(uint64_t)b[8] | ((uint64_t)b[9] << 32), (uint64_t)b[10] | ((uint64_t)b[11] << 32)};
+    }
+};
 // bytes y-8 .. y+39 (bytes outside the batch read 0)
 __device__ __forceinline__ void bytes48_chk(const uint8_t *p, int32_t y, V16 &c0, V16 &c1, V16 &c2, const uint8_t *lo,
                                             const uint8_t *hi) {
@@ -1170,16 +1273,17 @@ struct WindowFromSrc<LdsSrc> {
 // per SIMD), and at C2 one accepted copy in nine is 24 - 39 bytes long, whose exact extension
 // (gext_long) is a group-wide round trip that every stream of the wave waits for.
 constexpr int32_t kLCap = 40;
-template <class SRC>
+template <class SRC, bool LW = false>
 __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_t n, int32_t i, int32_t done, int64_t bs, int lj,
                                           int g, uint32_t *htw, uint32_t hsh, uint4 *rec, uint64_t rcap, const uint8_t *blo,
-                                          const uint8_t *bhi, int32_t &nrec_out, int &err) {
+                                          const uint8_t *bhi, int32_t &nrec_out, int &err, uint8_t *wl = nullptr) {
     constexpr int G = 16;
     int32_t nrec = 0;
     bool live = !err && i + 4 <= n;
     int64_t guard = 4 * (int64_t)n + 64;
     V16 w0{0, 0}, w1{0, 0}, w2{0, 0};  // bytes x-8 .. x+7, x+8 .. x+23, x+24 .. x+39 of this lane's position x
-    WinRollL wr;
+    typename std::conditional<LW, WinLdsL, WinRollL>::type wr;
+    if constexpr (LW) wr.wl = wl;
     if (!WindowFromSrc<SRC>::value) wr.init(p, i, lj, live, blo, bhi);
     constexpr bool kWinSrc = WindowFromSrc<SRC>::value;
 #if (EZ_EXP & 4)
@@ -1329,6 +1433,7 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
 // a group of 16 lanes per stream, 4 streams per wave; spec_mode 2: K1x's streams resume
 // spw: streams per wave (1, 2 or 4; the other lane groups idle, with no table): a batch of few long
 // streams runs more waves per SIMD, each a lone latency chain, instead of fewer waves of 4 streams
+template <bool LW = false>
 __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_words, uint4 *recs, uint64_t rcap, uint32_t spw) {
     constexpr int G = 16;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1356,7 +1461,10 @@ __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_wor
         for (int32_t k = lj; k < (int32_t)A.hs; k += G) htw[k] = have && spec ? A.spec_tab[s * (uint64_t)A.hs + k] : 0u;
     int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : (have ? 0 : EZ_EINVAL);
     int32_t nrec = 0;
-    long_loop(FreshSrc{{p, blo, bhi}}, p, n, i, done, A.bs, lj, g, htw, hsh, recs + (have ? s * rcap : 0), rcap, blo, bhi, nrec, err);
+    // (LW: the groups' window buffers after the tables)
+    uint8_t *wl = smem + (size_t)spw * table_words * 4 + (size_t)(grp ? g : 0) * kWinLdsBytes;
+    long_loop<FreshSrc, LW>(FreshSrc{{p, blo, bhi}}, p, n, i, done, A.bs, lj, g, htw, hsh, recs + (have ? s * rcap : 0), rcap, blo, bhi,
+                            nrec, err, wl);
     if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
 }
 
@@ -1459,7 +1567,7 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
 
 // FUSE: the wave writes its four streams' tokens itself after the parse (emit_stream, one stream at a
 // time by the whole wave), instead of a separate k1_emit launch reading the records back
-template <int TB, bool FUSE = false>
+template <int TB, bool FUSE = false, bool LW = false>
 __global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                  uint64_t rcap, int prio, uint8_t *edge) {
     constexpr int G = 16, S = 64 / G;
@@ -1505,7 +1613,9 @@ __global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, 
         __threadfence_block();
     }
     int32_t nrec = 0;
-    lean_loop<TB, !FUSE>(LeanIn{}, p, n, lj, g, hth, hsh, recw, roff, rcap, prio, nrec, err);
+    // (LW: the groups' window buffers after the four tables)
+    uint8_t *wl = smem + (size_t)4 * stride_words * S + (size_t)g * kWinLdsBytes;
+    lean_loop<TB, !FUSE, LW>(LeanIn{}, p, n, lj, g, hth, hsh, recw, roff, rcap, prio, nrec, err, wl);
     if (have && lj == 0) A.out_size[s] = (uint64_t)((EZ_EXP & 32768) ? 0 : nrec) | ((uint64_t)err << 48);
     if (FUSE) {
         // the records and counts this wave stored, visible to all its lanes (one wave, one CU: its
@@ -1780,7 +1890,19 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
         hipLaunchKernelGGL((k1_lean<16, true>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
         return hipGetLastError();
     }
-    if (t12)
+    // the window's region in LDS (WinLds; C1 K1 2.18 -> 2.08 ms, A/B on one box); EZ_K1S_LW=0 (A/B) keeps it in the lanes' registers
+    static const bool lw = knob("EZ_K1S_LW", 1) != 0;
+    if (lw && msk) {
+        static bool lattr = false;
+        if (!lattr) {
+            (void)hipFuncSetAttribute((const void *)k1_lean<12, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            (void)hipFuncSetAttribute((const void *)k1_lean<16, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+            lattr = true;
+        }
+        const size_t lds = (size_t)stride * 4 * S + (size_t)kWinLdsBytes * S + pad;
+        if (t12) hipLaunchKernelGGL((k1_lean<12, false, true>), dim3(grid), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
+        else hipLaunchKernelGGL((k1_lean<16, false, true>), dim3(grid), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
+    } else if (t12)
         hipLaunchKernelGGL(k1_lean<12>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
     else if (msk)
         hipLaunchKernelGGL(k1_lean<16>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
@@ -1938,14 +2060,18 @@ hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
     static const uint32_t spw_env = (uint32_t)knob("EZ_K1L_SPW", 0);
     const uint32_t S = spw_env == 1 || spw_env == 2 || spw_env == 4 ? spw_env : (a.count <= 256 ? 1u : 4u);
     const uint64_t rcap = rec_cap(a);
-    const size_t lds = (size_t)S * (size_t)a.hs * 4;
+    // the window's region in LDS (WinLdsL; C2 K1 25.8 -> 24.9 ms, C4s 254 -> 246); EZ_K1L_LW=0 (A/B) keeps it in registers
+    static const bool lw = knob("EZ_K1L_LW", 1) != 0;
+    const size_t lds = (size_t)S * (size_t)a.hs * 4 + (lw ? (size_t)S * kWinLdsBytes : 0);
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_long, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_long<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_long<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
-    hipLaunchKernelGGL(k1_long, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S);
+    if (lw) hipLaunchKernelGGL(k1_long<true>, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S);
+    else hipLaunchKernelGGL(k1_long<false>, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k1_emit<true>, dim3((unsigned)((a.count + 3) / 4)), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
