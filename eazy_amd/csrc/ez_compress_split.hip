@@ -1462,7 +1462,7 @@ __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_wor
     int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : (have ? 0 : EZ_EINVAL);
     int32_t nrec = 0;
     // (LW: the groups' window buffers after the tables)
-    uint8_t *wl = smem + (size_t)spw * table_words * 4 + (size_t)(grp ? g : 0) * kWinLdsBytes;
+    uint8_t *wl = smem + (size_t)spw * table_words * 4 + (size_t)g * kWinLdsBytes;  // (idle groups too: their own buffers)
     long_loop<FreshSrc, LW>(FreshSrc{{p, blo, bhi}}, p, n, i, done, A.bs, lj, g, htw, hsh, recs + (have ? s * rcap : 0), rcap, blo, bhi,
                             nrec, err, wl);
     if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
@@ -2062,7 +2062,7 @@ hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
     const uint64_t rcap = rec_cap(a);
     // the window's region in LDS (WinLdsL; C2 K1 25.8 -> 24.9 ms, C4s 254 -> 246); EZ_K1L_LW=0 (A/B) keeps it in registers
     static const bool lw = knob("EZ_K1L_LW", 1) != 0;
-    const size_t lds = (size_t)S * (size_t)a.hs * 4 + (lw ? (size_t)S * kWinLdsBytes : 0);
+    const size_t lds = (size_t)S * (size_t)a.hs * 4 + (lw ? (size_t)4 * kWinLdsBytes : 0);
     static bool attr_done = false;
     if (!attr_done) {
         (void)hipFuncSetAttribute((const void *)k1_long<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
