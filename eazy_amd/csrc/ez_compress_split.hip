@@ -1563,7 +1563,8 @@ __host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs 
 __host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs &a) { return 128 + kEdgeSlots * edge_slot_bytes(a) + 16; }
 
 template <bool WIDE>
-__device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane);
+__device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
+                                            uint64_t *stage = nullptr);
 
 // FUSE: the wave writes its four streams' tokens itself after the parse (emit_stream, one stream at a
 // time by the whole wave), instead of a separate k1_emit launch reading the records back
@@ -1643,13 +1644,15 @@ __device__ __forceinline__ void copy_lane(uint8_t *dst, const uint8_t *src, int3
 }
 
 constexpr int32_t kLongLit = 96;  // literals this long are copied by the whole wave
+constexpr int kEmitStage = 320;    // records of a stream staged in LDS by k1_emit (C1: ~220 per stream)
 
 // WIDE: k1_long's 16-byte records, and (spec_mode) the streams K1x hands over: their header and
 // first tokens are written already, the output continues at spec[s].op with the pending literal
 // from spec[s].done; streams K1x finished are skipped
 // the token writer of stream s (wave-uniform) by one wave
 template <bool WIDE>
-__device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane) {
+__device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
+                                            uint64_t *stage) {
     const bool spec = WIDE && A.spec_mode != 0;
     if (spec && A.spec[s].flags != 0) return;
     const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
@@ -1681,6 +1684,16 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
     }
     int32_t op = H, done = spec ? (int32_t)A.spec[s].done : 0;
     bool full = false;
+    // (stage: the stream's records in LDS, read with one round trip for all of them instead of one
+    // per 64-record chunk, each of which waited for the previous chunk's stores -- vmcnt is in order)
+    const bool staged = !WIDE && stage != nullptr && m <= kEmitStage;
+    if (!WIDE && staged) {
+        uint64_t t[kEmitStage / 64];
+#pragma unroll
+        for (int q = 0; q < kEmitStage / 64; q++) t[q] = q * 64 + lane < m ? rec[q * 64 + lane] : 0ull;
+#pragma unroll
+        for (int q = 0; q < kEmitStage / 64; q++) stage[q * 64 + lane] = t[q];
+    }
     for (int32_t b0 = 0; b0 < m && !full; b0 += 64) {
         const int32_t k = b0 + lane;
         const bool here = k < m;
@@ -1693,7 +1706,7 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
             dist = (int32_t)r4.z;
             forced = (r4.w & 1) != 0;
         } else {
-            const uint64_t r = here ? rec[k] : 0ull;
+            const uint64_t r = here ? (staged ? stage[k] : rec[k]) : 0ull;
             lit_end = (int32_t)(r & 0xfffff);
             clen = (int32_t)((r >> 20) & 0xfffff);
             dist = (int32_t)((r >> 40) & 0xfffff);
@@ -1785,11 +1798,13 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
 
 template <bool WIDE>
 __global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t *recs, uint64_t rcap) {
+    __shared__ uint64_t stage[WIDE ? 1 : 4][WIDE ? 1 : kEmitStage];
     const int lane = (int)(threadIdx.x & 63);
     // the wave's stream, wave-uniform (readfirstlane: its per-stream values live in SGPRs)
-    const uint64_t s = (uint64_t)blockIdx.x * 4 + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const uint64_t s = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
     if (s >= A.count) return;
-    emit_stream<WIDE>(A, recs, rcap, s, lane);
+    emit_stream<WIDE>(A, recs, rcap, s, lane, WIDE ? nullptr : &stage[WIDE ? 0 : w][0]);
 }
 
 // LDS words of a stream's table (0 = this variant cannot take the batch)
