@@ -259,6 +259,9 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         // past them, measured slower: 0.75 against 0.57 ms at C1)
         // (unflushed output stays below kChunk + 16 * (fper + 1) <= kRing bytes)
         if ((++it & (fper - 1)) == 0) {
+#if (EZ_EXP & (1 << 26))  // timing builds: no flush (wrong bytes)
+            if (it) {} else
+#endif
             while (any_lane(dst >= fl + kChunk)) {
                 if (dst >= fl + kChunk) {
 #pragma unroll
@@ -278,6 +281,9 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             const bool hn = rem > 0 && !patt && !near;
             const uint8_t *glo = from_in ? A.in : out, *ghi = from_in ? in_end : out + cap;
             const uint8_t *gc = !hn ? A.in : (sp < glo ? glo : (sp > ghi - 16 ? ghi - 16 : sp));
+#if (EZ_EXP & (1 << 25))  // timing builds: far copies read a line at the slot's start (wrong bytes; C1 only)
+            gc = hn && !from_in ? out + ((uint32_t)(sp - out) & 63) : gc;
+#endif
             graw = ld16v(gc);
             gd = (int32_t)(sp - gc);  // (hn lanes: the clamp's shift)
             sched_fence();            // (issued here, not sunk to the next iteration's parse)
