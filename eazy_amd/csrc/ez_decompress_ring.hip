@@ -116,6 +116,9 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
     // 32-bit positions; clamped loads need >= 16 input bytes in the batch and a 16-byte slot
     bool slow = in_end - A.in < 16 || nb64 >= (1ll << 30) || cap64 >= (1ll << 30) || cap64 < 16;
     const int32_t nb = slow ? 0 : (int32_t)nb64, cap = (int32_t)cap64;
+    // the batch's last 16-byte load position, relative to b (capped: a batch may pass 2 GiB)
+    const int64_t lh64 = (int64_t)(in_end - b) - 16;
+    const int32_t lit_hi = lh64 > 0x7fffffff ? 0x7fffffff : (int32_t)lh64;
     for (int32_t k = 0; k < kRing + 16; k += 16) {
         *(u64_ua *)(ring + k) = 0;
         *(u64_ua *)(ring + k + 8) = 0;
@@ -136,11 +139,14 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             h = ld_in(b, A.in, in_end);
         }
     }
-    // the token being written: rem bytes at dst from sp (input / HBM output) or from the ring
+    // the token being written: rem bytes at dst from sb + so (input / HBM output; 32-bit offsets,
+    // loads clamped to [sb, sb + shi + 16)) or from the ring
     int32_t rem = 0, dst = 0, step = 16, rp = 0, fl = 0;  // fl: output below it is in HBM
     uint32_t it = 0;
-    const uint8_t *sp = b;
-    bool from_in = false, patt = false, near = false, live = !slow;
+    const uint8_t *sb = b;
+    int32_t so = 0, shi = lit_hi;
+    int32_t src = 0;  // the move's bytes: 0 from HBM (a far copy, a long literal), 1 the pattern pv, 2 the ring
+    bool live = !slow;
     V16 pv{0, 0};
     // (a load after the first header, as every iteration ends with one after the next header:
     // the loop's entry then matches its back edge and the header wait counts past it; the
@@ -163,7 +169,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         // ---- move, part 1: this iteration's bytes of the current token (rem == 0: nothing);
         // a far copy's or long literal's 16 bytes (graw) were loaded one iteration ago
         V16 v = ring_ld(ring, rp);
-        const bool hb = rem > 0 && !patt && !near;  // a far copy or a long literal: from HBM
+        const bool hb = rem > 0 && src == 0;  // a far copy or a long literal: from HBM
         const int32_t kk = rem < step ? rem : step;
         // ---- parse: the lanes whose current token ends with this move take the next one
         bool np = live && rem == kk;
@@ -217,9 +223,9 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             }
             hd = (int32_t)(y - wb);
         } else {
-            const uint8_t *hc = b + i > in_end - 16 ? in_end - 16 : b + i;  // (the batch's last 16 bytes)
-            h = ld16v(hc);
-            hd = (int32_t)(b + i - hc);
+            const int32_t ic = i < lit_hi ? i : lit_hi;  // (the batch's last 16 bytes)
+            h = ld16v(b + ic);
+            hd = i - ic;
         }
         // ---- move, part 2
         V16 g = graw;
@@ -228,23 +234,23 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         }
         v.lo = hb ? g.lo : v.lo;  // (field by field: a select of the struct went through scratch)
         v.hi = hb ? g.hi : v.hi;
-        v.lo = patt ? pv.lo : v.lo;
-        v.hi = patt ? pv.hi : v.hi;
+        v.lo = src == 1 ? pv.lo : v.lo;
+        v.hi = src == 1 ? pv.hi : v.hi;
         ring_st(ring, dst, v);
         dst += kk;
-        sp += kk;
+        so += kk;
         rp += kk;
         rem -= kk;
         // ---- the next token's state (a padding or meta step has L = 0: no move)
         const bool run = cp && D < 16;
         rem = np ? L : rem;
-        from_in = np ? !cp : from_in;
-        near = np ? cp && D <= kNear : near;
         rp = np ? pos - (int32_t)D : rp;
-        sp = np ? (cp ? out + (pos - (int32_t)D) : b + (i0 + j)) : sp;
+        so = np ? (cp ? pos - (int32_t)D : i0 + j) : so;
+        sb = np ? (cp ? (const uint8_t *)out : b) : sb;
+        shi = np ? (cp ? cap - 16 : lit_hi) : shi;
         // zero region (D == 0, reader.go:176-179) or a short-period run: one 16-byte pattern
         // stored every `step` bytes; a short literal is in the header's 16 bytes already
-        patt = np ? run || (!cp && j + L <= 16) : patt;
+        src = np ? (run || (!cp && j + L <= 16) ? 1 : (cp && D <= kNear ? 2 : 0)) : src;
         step = np ? (run ? run_step(D) : 16) : step;
         pv.lo = np ? hv.lo : pv.lo;
         pv.hi = np ? hv.hi : pv.hi;
@@ -278,14 +284,16 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         // wait; A.in for the others, the batch holds >= 16 bytes when any lane is live), so the
         // next iteration's parse and header load run while it is in flight
         {
-            const bool hn = rem > 0 && !patt && !near;
-            const uint8_t *glo = from_in ? A.in : out, *ghi = from_in ? in_end : out + cap;
-            const uint8_t *gc = !hn ? A.in : (sp < glo ? glo : (sp > ghi - 16 ? ghi - 16 : sp));
+            const bool hn = rem > 0 && src == 0;
+            int32_t sc = so > 0 ? so : 0;
+            sc = sc < shi ? sc : shi;  // (a copy before the slot's start, a literal at the batch's end)
+            // (the others all load the batch's first line: one line per wave instead of a gather)
+            const uint8_t *gc = hn ? sb + sc : A.in;
 #if (EZ_EXP & (1 << 25))  // timing builds: far copies read a line at the slot's start (wrong bytes; C1 only)
-            gc = hn && !from_in ? out + ((uint32_t)(sp - out) & 63) : gc;
+            gc = hn && sb == out ? out + ((uint32_t)so & 63) : gc;
 #endif
             graw = ld16v(gc);
-            gd = (int32_t)(sp - gc);  // (hn lanes: the clamp's shift)
+            gd = so - sc;  // (hn lanes: the clamp's shift)
             sched_fence();            // (issued here, not sunk to the next iteration's parse)
         }
     }
