@@ -99,6 +99,17 @@ def test_ragged_and_edge_lengths(cuda):
     _check(cuda, bufs)
 
 
+def test_tiny_streams_at_batch_end(cuda):
+    """The last streams start within the batch's final 16 bytes: K2r's header and literal loads
+    are clamped to the batch's last 16 bytes (bytes past it read as 0), every decoder agrees."""
+    from eazy_amd import synth
+
+    d = synth.logs(13, 64 * 4096).tobytes()
+    tail = [b"a", b"xyz", b"0123456789abcdef0", b"", b"q"]
+    _check(cuda, [d[k * 4096 : (k + 1) * 4096] for k in range(64)] + tail)
+    _check(cuda, [b"z"] + tail)
+
+
 def test_many_streams_k1l_and_long_slots(cuda):
     """Batches past 256 streams: K1L (when forced) runs 4 streams per wave, up to 256
     one; and >= 12,288 streams with 64 KiB slots take the lane-per-stream decoder K2r by
