@@ -514,10 +514,11 @@ def main():
     from eazy_amd import synth
 
     world, rank, local = R.world, R.rank, R.local
-    if world > 1:
-        dist.init_process_group("nccl")
+    # the rank's device is bound before RCCL starts, and named to it (no guess from the rank)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
 
     wl = args.workload if args.workload != "auto" else ("c1" if world == 1 else "c3")
     count, size, block, htable, desc = WORKLOADS[wl]

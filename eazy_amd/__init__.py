@@ -169,15 +169,14 @@ def select_compress_kernel(kind: str = "") -> None:
 
 
 def select_decompress_kernel(kind: str = "") -> None:
-    """Force the first K2 kernel of later batch decodes ('s' token walk + 16 lanes per stream,
-    slots <= 4 KiB; 'r' ring, 't' token-parallel wave per stream, 'w' wave per stream; '' =
-    automatic).  Tests and A/B measurement only."""
+    """Force the first K2 kernel of later batch decodes ('r' ring, 't' token-parallel wave per
+    stream, 'w' wave per stream; '' = automatic).  Tests and A/B measurement only."""
     _check(_lib().ez_select_decompress_kernel(ord(kind) if kind else 0))
 
 
 def decompress_kernel_last() -> str:
-    """The first K2 kernel the last batch decode of this process ran ('s', 'r', 't', 'w'; 'e'
-    the exact decoder alone; '' none yet)."""
+    """The first K2 kernel the last batch decode of this process ran ('r', 't', 'w'; 'e' the
+    exact decoder alone; '' none yet)."""
     v = _lib().ez_decompress_kernel_last()
     return chr(v) if v else ""
 
@@ -589,6 +588,64 @@ def compress_batch(data, in_off, block: int = MiB, htable: int = 1024, max_len: 
     flags = 0 if append_magic else F_NO_MAGIC
     _check(_lib().ez_compress_batch(block, htable, flags, C.byref(b), _stream_ptr(stream)))
     return out
+
+
+def _host_u8(b) -> "np.ndarray":
+    import numpy as np
+
+    if isinstance(b, np.ndarray):
+        return np.ascontiguousarray(b, dtype=np.uint8).reshape(-1)
+    return np.frombuffer(bytes(b), dtype=np.uint8)
+
+
+def compress_batch_multi(data, in_off, block: int = MiB, htable: int = 1024, devices=None,
+                         append_magic: bool = True):
+    """Host-memory batch over several devices (ez_compress_batch_multi): stream s =
+    data[in_off[s]:in_off[s+1]] (numpy uint8 / int64, or bytes) as one Write to a fresh
+    NewWriter(block, htable), compressed in contiguous whole-stream shards, one per entry of
+    `devices` (None: every visible device; repeats allowed).  Returns (packed bytes, packed
+    offsets int64[count+1], statuses int32[count])."""
+    import numpy as np
+
+    d = _host_u8(data)
+    off = np.ascontiguousarray(in_off, dtype=np.uint64)
+    count = len(off) - 1
+    n = off[1:].astype(np.int64) - off[:-1].astype(np.int64)
+    cap = int(np.sum(n + (n >> 2) + 32)) + 16
+    packed = np.empty(max(cap, 1), np.uint8)
+    poff = np.zeros(count + 1, np.uint64)
+    status = np.zeros(max(count, 1), np.int32)
+    devs = None if devices is None else (C.c_int * len(devices))(*devices)
+    L = _lib()
+    L.ez_compress_batch_multi.argtypes = [C.c_int64, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p,
+                                          C.c_int, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    _check(L.ez_compress_batch_multi(block, htable, 0 if append_magic else F_NO_MAGIC, d.ctypes.data, off.ctypes.data, count,
+                                     devs, len(devices) if devices else 0, packed.ctypes.data, cap, poff.ctypes.data,
+                                     status.ctypes.data))
+    return packed[: int(poff[-1])], poff.astype(np.int64), status[:count]
+
+
+def decompress_batch_multi(comp, comp_off, out_off, block_size_limit: int = 0, devices=None):
+    """Host-memory decode over several devices (ez_decompress_batch_multi): stream s =
+    comp[comp_off[s]:comp_off[s+1]] read to EOF into out[out_off[s]:out_off[s+1]].  Returns
+    (out bytes, sizes int64[count], statuses int32[count])."""
+    import numpy as np
+
+    c = _host_u8(comp)
+    coff = np.ascontiguousarray(comp_off, dtype=np.uint64)
+    ooff = np.ascontiguousarray(out_off, dtype=np.uint64)
+    count = len(coff) - 1
+    out = np.zeros(max(int(ooff[-1]), 1), np.uint8)
+    sizes = np.zeros(max(count, 1), np.uint64)
+    status = np.zeros(max(count, 1), np.int32)
+    devs = None if devices is None else (C.c_int * len(devices))(*devices)
+    L = _lib()
+    L.ez_decompress_batch_multi.argtypes = [C.c_int64, C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int, C.c_void_p,
+                                            C.c_void_p, C.c_void_p, C.c_void_p]
+    _check(L.ez_decompress_batch_multi(block_size_limit, c.ctypes.data, coff.ctypes.data, count, devs,
+                                       len(devices) if devices else 0, out.ctypes.data, ooff.ctypes.data, sizes.ctypes.data,
+                                       status.ctypes.data))
+    return out[: int(ooff[-1])], sizes[:count].astype(np.int64), status[:count]
 
 
 def compress_batch_writes(data, in_off, write_idx, write_end, block: int = MiB, htable: int = 1024,

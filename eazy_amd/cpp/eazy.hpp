@@ -669,4 +669,65 @@ inline Err DecompressBatch(int64_t block_size_limit, const ez_batch &b, void *wo
     return (Err)ez_decompress_batch(block_size_limit, &b, workspace, hip_stream);
 }
 
+// Host-memory batches over several devices (ez_compress_batch_multi / ez_decompress_batch_multi):
+// bufs[k] is one Write to a fresh NewWriter(block, htable); out[k] gets its compressed bytes,
+// computed in contiguous whole-stream shards, one per entry of `devices` (empty: every device).
+// Err::Device without a usable device; a stream's own error otherwise (the first one).
+inline Err CompressBatchMulti(const std::vector<std::vector<uint8_t>> &bufs, int64_t block, int64_t htable,
+                              std::vector<std::vector<uint8_t>> &out, const std::vector<int> &devices = {},
+                              bool append_magic = true) {
+    detail::size_panic(block, htable);
+    std::vector<uint64_t> off(bufs.size() + 1, 0);
+    uint64_t cap = 16;
+    for (size_t k = 0; k < bufs.size(); k++) {
+        off[k + 1] = off[k] + bufs[k].size();
+        cap += ez_compress_bound(bufs[k].size());
+    }
+    std::vector<uint8_t> in;
+    in.reserve(off.back());
+    for (const auto &b : bufs) in.insert(in.end(), b.begin(), b.end());
+    std::vector<uint8_t> packed(cap);
+    std::vector<uint64_t> poff(bufs.size() + 1, 0);
+    std::vector<int32_t> status(bufs.size() + 1, 0);
+    const int st = ez_compress_batch_multi(block, htable, append_magic ? 0 : EZ_F_NO_MAGIC, in.data(), off.data(), bufs.size(),
+                                           devices.empty() ? nullptr : devices.data(), (int)devices.size(), packed.data(), cap,
+                                           poff.data(), status.data());
+    if (st == EZ_EINVAL) throw std::invalid_argument("eazy: CompressBatchMulti: invalid arguments");
+    if (st != EZ_OK) return (Err)st;
+    out.assign(bufs.size(), {});
+    for (size_t k = 0; k < bufs.size(); k++) {
+        if (status[k] != EZ_OK) return (Err)status[k];
+        out[k].assign(packed.begin() + (ptrdiff_t)poff[k], packed.begin() + (ptrdiff_t)poff[k + 1]);
+    }
+    return Err::OK;
+}
+
+// Every stream read to EOF (NewReaderBytes; Break metas skipped) into a slot of slot_bytes[k]
+// bytes: out[k] = (its output, its first error or OK).
+inline Err DecompressBatchMulti(const std::vector<std::vector<uint8_t>> &streams, const std::vector<uint64_t> &slot_bytes,
+                                std::vector<std::pair<std::vector<uint8_t>, Err>> &out, const std::vector<int> &devices = {},
+                                int64_t block_size_limit = 0) {
+    if (slot_bytes.size() != streams.size()) throw std::invalid_argument("eazy: DecompressBatchMulti: one slot per stream");
+    std::vector<uint64_t> off(streams.size() + 1, 0), ooff(streams.size() + 1, 0);
+    for (size_t k = 0; k < streams.size(); k++) {
+        off[k + 1] = off[k] + streams[k].size();
+        ooff[k + 1] = ooff[k] + slot_bytes[k];
+    }
+    std::vector<uint8_t> in;
+    in.reserve(off.back());
+    for (const auto &b : streams) in.insert(in.end(), b.begin(), b.end());
+    std::vector<uint8_t> buf(ooff.back() + 1);
+    std::vector<uint64_t> sizes(streams.size() + 1, 0);
+    std::vector<int32_t> status(streams.size() + 1, 0);
+    const int st = ez_decompress_batch_multi(block_size_limit, in.data(), off.data(), streams.size(),
+                                             devices.empty() ? nullptr : devices.data(), (int)devices.size(), buf.data(), ooff.data(),
+                                             sizes.data(), status.data());
+    if (st == EZ_EINVAL) throw std::invalid_argument("eazy: DecompressBatchMulti: invalid arguments");
+    if (st != EZ_OK) return (Err)st;
+    out.assign(streams.size(), {});
+    for (size_t k = 0; k < streams.size(); k++)
+        out[k] = {std::vector<uint8_t>(buf.begin() + (ptrdiff_t)ooff[k], buf.begin() + (ptrdiff_t)(ooff[k] + sizes[k])), (Err)status[k]};
+    return Err::OK;
+}
+
 }  // namespace eazy

@@ -11,7 +11,10 @@
 
 #include <map>
 #include <mutex>
+#include <algorithm>
 #include <vector>
+#include <memory>
+#include <thread>
 
 #include "ez_format.h"
 #include "ez_internal.h"
@@ -598,13 +601,19 @@ struct ez_reader {
     DBuf in, obuf[2], dstate, meta;  // obuf: history + output, double-buffered (ez_reader_read)
     int cur = 0;
     hipStream_t stream = nullptr;
-    // whole-buffer decode-ahead (ez_reader_set_whole): the stream decoded once by the batch path,
-    // the Reads served from `ahead`
-    int whole = 0;          // the caller's b is the whole stream (NewReaderBytes / ResetBytes)
-    int tried = 0;          // decode-ahead tried since the last reset
-    int ahead_on = 0;       // Reads are served from ahead[ahead_at .. ahead.size())
-    std::vector<uint8_t> ahead;
-    size_t ahead_at = 0;
+    // whole-stream decode (ez_reader_set_whole): the stream decoded once by the batch path into a_out
+    // (device memory), the Reads served from it through a pinned staging window
+    int whole = 0;             // the caller's b is the whole stream (NewReaderBytes / ResetBytes)
+    int tried = 0;             // tried since the last reset
+    int ahead_on = 0;          // Reads are served from a_out[a_at .. a_n)
+    DBuf a_in, a_out, a_meta, a_ws, a_brk;  // kept across resets (grown, never shrunk)
+    uint64_t a_n = 0, a_at = 0;             // bytes decoded; bytes served
+    size_t a_blen = 0;                      // the input decoded (len(r.b) at the first Read)
+    std::vector<uint64_t> brk;              // the Break metas' output positions, ascending
+    size_t brk_next = 0;                    // the next one a Read has not reported
+    int64_t end_bs = 0, end_pos = 0;        // the Reader's len(r.block) and r.pos after the stream
+    uint8_t *stage = nullptr;               // pinned: a_out[stage_at .. stage_at + stage_n)
+    uint64_t stage_at = 0, stage_n = 0;
 };
 
 extern "C" int ez_reader_new(int device, ez_reader **out) {
@@ -633,6 +642,12 @@ extern "C" void ez_reader_free(ez_reader *r) {
     r->obuf[1].release();
     r->dstate.release();
     r->meta.release();
+    r->a_in.release();
+    r->a_out.release();
+    r->a_meta.release();
+    r->a_ws.release();
+    r->a_brk.release();
+    if (r->stage) (void)hipHostFree(r->stage);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
 }
@@ -652,9 +667,10 @@ extern "C" int ez_reader_reset(ez_reader *r) {
     r->st.ver = ver;
     r->tried = 0;
     r->ahead_on = 0;
-    r->ahead.clear();
-    r->ahead.shrink_to_fit();
-    r->ahead_at = 0;
+    r->a_n = r->a_at = 0;
+    r->brk.clear();
+    r->brk_next = 0;
+    r->stage_n = 0;
     return EZ_OK;
 }
 
@@ -668,59 +684,134 @@ extern "C" int ez_reader_whole_decoded(const ez_reader *r) { return r->ahead_on;
 extern "C" int ez_reader_pending(const ez_reader *r) { return r->st.state != 0 ? 1 : 0; }
 
 namespace {
-// Decode-ahead of a whole stream (NewReaderBytes then Read to the end, the reference's common use):
-// the batch path decodes b as one stream -- K2t, every lane of a wave on its tokens -- into a slot of
-// up to 8 x b_len bytes, and the Reads are then served from that output.  It applies only where Read
-// by Read decoding gives exactly those bytes and nothing else: a clean end of stream (status OK) and
-// no Break meta (Read reports ErrBreak there, the batch path skips it), with RequireMagic and
-// SkipUnsupportedMeta off; anything else leaves the handle as it was and the exact decoder runs Read
-// by Read.  Returns 1 when the Reads are now served from the decoded bytes.
+constexpr size_t kAheadMax = ((size_t)1 << 30) - 64;  // the largest output slot (K2t takes slots below 2^30)
+constexpr size_t kAheadBrk = (size_t)1 << 16;         // Break positions recorded (more: Read by Read)
+constexpr size_t kStage = (size_t)4 << 20;            // the pinned staging window (host memory per Reader)
+
+// Whole-stream decode (NewReaderBytes then Read to the end, the reference's common use): the batch
+// path decodes b as one stream -- K2t, every lane of a wave on its tokens -- into a device slot, and the
+// Reads are then served from that output.  The slot starts at 8 x b_len and grows 4x while K2t reports
+// it too small (up to 1 GiB).  The decoders record every Break meta's output position, so the Reads stop
+// at each with ErrBreak as Read by Read does (reader.go:312-313), and the Reader's state at the end
+// (len(r.block), r.pos), so that input a caller supplies after the stream (a Reader set after
+// NewReaderBytes) continues Read by Read.  It applies where it gives exactly the bytes and errors of
+// Read-by-Read decoding: a clean end of stream (status OK), RequireMagic and SkipUnsupportedMeta off;
+// anything else leaves the handle as it was and the exact decoder runs Read by Read.  Device buffers are
+// kept in the handle, host memory is the 4 MiB staging window.  Returns 1 when the Reads are now
+// served from the decoded bytes.
 int reader_ahead(ez_reader *r, const uint8_t *b, size_t b_len) {
     r->tried = 1;
     if (b_len == 0 || b_len > ((size_t)1 << 28) || r->require_magic || r->skip_meta) return 0;
-    const size_t cap = 8 * b_len + 4096 < ((size_t)1 << 30) ? 8 * b_len + 4096 : ((size_t)1 << 30);
-    DBuf din, dout, dm, dws;
     const size_t ws = ez_decompress_workspace(1);
-    const size_t o_meta = 64;
-    if (din.ensure(b_len + 64) || dout.ensure(cap + 64) || dm.ensure(o_meta + 8 * 8) || dws.ensure(ws)) return 0;
-    uint64_t m[8] = {0, (uint64_t)b_len, 0, (uint64_t)cap, 0, 0, 0, 0};  // in_off, out_off, out_size, status, breaks
-    int ok = 0;
-    do {
-        if (hipMemcpyAsync(din.p, b, b_len, hipMemcpyHostToDevice, r->stream) != hipSuccess) break;
-        if (hipMemcpyAsync(dm.p, m, sizeof m, hipMemcpyHostToDevice, r->stream) != hipSuccess) break;
-        uint64_t *dmw = dm.as<uint64_t>();
+    constexpr size_t o_meta = 64;  // [in_off 2][out_off 2][out_size][status][end_state 2]
+    if (r->a_in.ensure(b_len + 64) || r->a_meta.ensure(o_meta * 2) || r->a_ws.ensure(ws) || r->a_brk.ensure(8 * (kAheadBrk + 1)))
+        return 0;
+    if (!r->stage && hipHostMalloc((void **)&r->stage, kStage, hipHostMallocDefault) != hipSuccess) {
+        r->stage = nullptr;
+        return 0;
+    }
+    if (hipMemcpyAsync(r->a_in.p, b, b_len, hipMemcpyHostToDevice, r->stream) != hipSuccess) return 0;
+    size_t cap = 8 * b_len + 4096 < kAheadMax ? 8 * b_len + 4096 : kAheadMax;
+    for (;;) {
+        if (r->a_out.ensure(cap + 64)) return 0;
+        uint64_t m[8] = {0, (uint64_t)b_len, 0, (uint64_t)cap, 0, 0, (uint64_t)-1, (uint64_t)-1};
+        uint64_t nbrk = 0;
+        if (hipMemcpyAsync(r->a_meta.p, m, sizeof m, hipMemcpyHostToDevice, r->stream) != hipSuccess) return 0;
+        if (hipMemsetAsync(r->a_brk.p, 0, 8, r->stream) != hipSuccess) return 0;
+        uint64_t *dmw = r->a_meta.as<uint64_t>();
         ez::DecompressArgs a{};
-        a.in = din.as<uint8_t>();
+        a.in = r->a_in.as<uint8_t>();
         a.in_off = dmw;
-        a.out = dout.as<uint8_t>();
+        a.out = r->a_out.as<uint8_t>();
         a.out_off = dmw + 2;
         a.out_size = dmw + 4;
         a.status = (int32_t *)(dmw + 5);
-        a.breaks = (uint32_t *)(dmw + 6);
+        a.end_state = (int64_t *)(dmw + 6);
+        a.breaks = r->a_brk.as<uint64_t>();
+        a.breaks_cap = kAheadBrk;
         a.count = 1;
         a.block_size_limit = r->limit;
-        a.slow = dws.as<uint32_t>();
+        a.slow = r->a_ws.as<uint32_t>();
         a.max_out = cap;
         a.force = 't';  // one stream: the token-parallel wave
-        if (ez::launch_decompress(a, r->stream) != hipSuccess) break;
-        if (hipMemcpyAsync(m, dm.p, sizeof m, hipMemcpyDeviceToHost, r->stream) != hipSuccess) break;
-        if (hipStreamSynchronize(r->stream) != hipSuccess) break;
-        if ((int32_t)(m[5] & 0xffffffffu) != EZ_OK || (uint32_t)m[6] != 0 || m[4] > cap) break;
-        r->ahead.resize((size_t)m[4]);
-        if (m[4] && hipMemcpy(r->ahead.data(), dout.p, (size_t)m[4], hipMemcpyDeviceToHost) != hipSuccess) break;
-        r->ahead_at = 0;
+        if (ez::launch_decompress(a, r->stream) != hipSuccess) return 0;
+        if (hipMemcpyAsync(m, r->a_meta.p, sizeof m, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
+        if (hipMemcpyAsync(&nbrk, r->a_brk.p, 8, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
+        if (hipStreamSynchronize(r->stream) != hipSuccess) return 0;
+        const int status = (int32_t)(m[5] & 0xffffffffu);
+        if ((int64_t)m[6] == -2 && status == EZ_ENOSPC && cap < kAheadMax) {  // the slot was too small
+            cap = cap < kAheadMax / 4 ? 4 * cap : kAheadMax;
+            continue;
+        }
+        if (status != EZ_OK || m[4] > cap || nbrk > kAheadBrk || (int64_t)m[6] < 0) return 0;
+        try {
+            r->brk.resize((size_t)nbrk);
+        } catch (...) {
+            return 0;
+        }
+        if (nbrk && (hipMemcpy(r->brk.data(), r->a_brk.as<uint64_t>() + 1, 8 * nbrk, hipMemcpyDeviceToHost) != hipSuccess)) {
+            r->brk.clear();
+            return 0;
+        }
+        std::sort(r->brk.begin(), r->brk.end());
+        r->brk_next = 0;
+        r->a_n = m[4];
+        r->a_at = 0;
+        r->a_blen = b_len;
+        r->end_bs = (int64_t)m[6];
+        r->end_pos = (int64_t)m[7];
+        r->stage_at = r->stage_n = 0;
         r->ahead_on = 1;
-        ok = 1;
-    } while (0);
-    if (!ok) {
-        r->ahead.clear();
-        r->ahead.shrink_to_fit();
+        return 1;
     }
-    din.release();
-    dout.release();
-    dm.release();
-    dws.release();
-    return ok;
+}
+
+// n bytes of the decoded stream from a_at into p (staged; a copy larger than the window goes direct)
+int ahead_copy(ez_reader *r, uint8_t *p, size_t n) {
+    while (n) {
+        if (r->a_at < r->stage_at || r->a_at >= r->stage_at + r->stage_n) {
+            const uint64_t left = r->a_n - r->a_at;
+            if (n >= kStage) {
+                if (hipMemcpy(p, r->a_out.as<uint8_t>() + r->a_at, n, hipMemcpyDeviceToHost) != hipSuccess) return EZ_EDEVICE;
+                r->a_at += n;
+                return EZ_OK;
+            }
+            r->stage_at = r->a_at;
+            r->stage_n = left < kStage ? left : kStage;
+            if (hipMemcpy(r->stage, r->a_out.as<uint8_t>() + r->a_at, r->stage_n, hipMemcpyDeviceToHost) != hipSuccess) {
+                r->stage_n = 0;
+                return EZ_EDEVICE;
+            }
+        }
+        const uint64_t in_stage = r->stage_at + r->stage_n - r->a_at;
+        const size_t k = n < in_stage ? n : (size_t)in_stage;
+        memcpy(p, r->stage + (r->a_at - r->stage_at), k);
+        p += k;
+        n -= k;
+        r->a_at += k;
+    }
+    return EZ_OK;
+}
+
+// Input after the decoded stream (a Reader set after NewReaderBytes, so more() supplied more): the
+// handle continues Read by Read from the Reader's state at the stream's end -- len(r.block), r.pos, no
+// token pending, version 0 (the whole decode takes only those) -- with the window's history, the last
+// min(r.pos, len(r.block)) decoded bytes, at the head of the decode buffer.
+int ahead_leave(ez_reader *r) {
+    ez::DecodeState st{};
+    st.bs = r->end_bs;
+    st.pos = r->end_pos;
+    st.hist = st.bs == 0 ? 0 : (st.pos < st.bs ? st.pos : st.bs);
+    const size_t H = (size_t)st.hist;
+    if (H > r->a_n) return EZ_EDEVICE;  // (cannot happen: the history is decoded output)
+    DBuf &cur = r->obuf[r->cur];
+    if (cur.ensure(H + 16)) return EZ_EDEVICE;
+    if (H && hipMemcpyAsync(cur.p, r->a_out.as<uint8_t>() + (r->a_n - H), H, hipMemcpyDeviceToDevice, r->stream) != hipSuccess)
+        return EZ_EDEVICE;
+    if (hipStreamSynchronize(r->stream) != hipSuccess) return EZ_EDEVICE;
+    r->st = st;
+    r->ahead_on = 0;
+    return EZ_OK;
 }
 }  // namespace
 
@@ -742,13 +833,25 @@ extern "C" int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size
     // a fresh handle over a whole stream: decode it once (reader_ahead), then serve every Read from it
     if (!r->ahead_on && r->whole && !r->tried && i == 0 && boff == 0 && r->st.bs == 0 && r->st.pos == 0 && r->st.state == 0)
         (void)reader_ahead(r, b, b_len);
+    if (r->ahead_on && r->a_at == r->a_n && r->brk_next == r->brk.size() && (uint64_t)boff + b_len > r->a_blen) {
+        // the stream is served and input follows it: Read by Read from the Reader's state at its end
+        if (ahead_leave(r) != EZ_OK) return EZ_EDEVICE;
+    }
     if (r->ahead_on) {
-        const size_t left = r->ahead.size() - r->ahead_at, m = p_len < left ? p_len : left;
-        if (m) memcpy(p, r->ahead.data() + r->ahead_at, m);
-        r->ahead_at += m;
+        // up to the next Break (reader.go:312-313: Read returns the bytes before it with ErrBreak, and a
+        // Read that starts at it returns 0 bytes with ErrBreak) or the stream's end
+        const bool at_brk = r->brk_next < r->brk.size();
+        const uint64_t lim = at_brk ? r->brk[r->brk_next] : r->a_n;
+        const uint64_t left = lim - r->a_at;
+        const size_t m = p_len < left ? p_len : (size_t)left;
+        if (m && ahead_copy(r, p, m) != EZ_OK) return EZ_EDEVICE;
         *n = m;
         if (m == p_len) return EZ_OK;  // (the input position is reported when the output is done)
-        *i_out = b_len;                 // the stream's end: Read asks for more input and gets EOF
+        if (at_brk) {
+            r->brk_next++;
+            return EZ_EBREAK;
+        }
+        *i_out = b_len;  // the stream's end: Read asks for more input and gets EOF
         return EZ_ESHORTBUF;
     }
     const size_t H = (size_t)r->st.hist;
@@ -908,7 +1011,7 @@ extern "C" int ez_select_compress_kernel(int kind) {
 }
 
 extern "C" int ez_select_decompress_kernel(int kind) {
-    if (kind != 0 && kind != 's' && kind != 'r' && kind != 'w' && kind != 't') return EZ_EINVAL;
+    if (kind != 0 && kind != 'r' && kind != 'w' && kind != 't') return EZ_EINVAL;
     ez::select_decompress_variant(kind);
     return EZ_OK;
 }
@@ -935,4 +1038,207 @@ extern "C" int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, 
     a.max_out = b->max_len;  // decompress: the largest output slot, if the caller knows it
     EZ_HIP(ez::launch_decompress(a, (hipStream_t)hip_stream));
     return EZ_OK;
+}
+
+// ------------------------------------------------------------------ host batches over several devices
+
+namespace {
+// Contiguous whole-stream shards of a batch, balanced by bytes: shard k is streams [first[k],
+// first[k+1]) with first[k] the first stream starting at or after k / nshard of the batch's bytes.
+std::vector<uint64_t> shard_bounds(const uint64_t *off, uint64_t count, int nshard) {
+    std::vector<uint64_t> first((size_t)nshard + 1, count);
+    first[0] = 0;
+    const uint64_t total = off[count] - off[0];
+    uint64_t s = 0;
+    for (int k = 1; k < nshard; k++) {
+        const uint64_t target = off[0] + (uint64_t)((unsigned __int128)total * (uint64_t)k / (uint64_t)nshard);
+        while (s < count && off[s] < target) s++;
+        first[(size_t)k] = s;
+    }
+    return first;
+}
+
+int resolve_devices(const int *devices, int ndev, std::vector<int> &out) {
+    const int have = device_count();
+    if (have <= 0) return EZ_EDEVICE;
+    if (!devices || ndev <= 0) {
+        for (int d = 0; d < have; d++) out.push_back(d);
+        return EZ_OK;
+    }
+    for (int k = 0; k < ndev; k++) {
+        if (devices[k] < 0 || devices[k] >= have) return EZ_EINVAL;
+        out.push_back(devices[k]);
+    }
+    return EZ_OK;
+}
+
+// one shard's device buffers and HIP stream (its host thread owns them)
+struct Shard {
+    int dev = 0;
+    uint64_t first = 0, count = 0;
+    hipStream_t st = nullptr;
+    DBuf in, in_off, out, out_off, size, status, ws, packed, packed_off;
+    uint64_t total = 0, base = 0;  // compress: packed bytes of the shard, its place in the global packing
+    int err = EZ_OK;
+    ~Shard() {
+        if (dev >= 0) (void)hipSetDevice(dev);
+        for (DBuf *b : {&in, &in_off, &out, &out_off, &size, &status, &ws, &packed, &packed_off}) b->release();
+        if (st) (void)hipStreamDestroy(st);
+    }
+};
+
+// run f(shard) on one host thread per shard (each binds its device first) and join them
+template <class F>
+int each_shard(std::vector<std::unique_ptr<Shard>> &sh, F f) {
+    std::vector<std::thread> th;
+    for (auto &p : sh) {
+        Shard *x = p.get();
+        if (x->count == 0) continue;
+        th.emplace_back([x, &f]() {
+            if (hipSetDevice(x->dev) != hipSuccess) {
+                x->err = EZ_EDEVICE;
+                return;
+            }
+            if (!x->st && hipStreamCreateWithFlags(&x->st, hipStreamNonBlocking) != hipSuccess) {
+                x->st = nullptr;
+                x->err = EZ_EDEVICE;
+                return;
+            }
+            if (x->err == EZ_OK) x->err = f(*x);
+        });
+    }
+    for (auto &t : th) t.join();
+    for (auto &p : sh)
+        if (p->err != EZ_OK) return p->err;
+    return EZ_OK;
+}
+}  // namespace
+
+#define EZ_SHARD_HIP(x)                          \
+    do {                                         \
+        if ((x) != hipSuccess) return EZ_EDEVICE; \
+    } while (0)
+
+extern "C" int ez_compress_batch_multi(int64_t block, int64_t htable, int flags, const uint8_t *in, const uint64_t *in_off,
+                                       uint64_t count, const int *devices, int ndev, uint8_t *packed, uint64_t packed_cap,
+                                       uint64_t *packed_off, int32_t *status) {
+    if (!valid_writer_sizes(block, htable) || !in_off || !packed_off) return EZ_EINVAL;
+    std::vector<int> devs;
+    int e = resolve_devices(devices, ndev, devs);
+    if (e != EZ_OK) return e;
+    packed_off[0] = 0;
+    if (count == 0) return EZ_OK;
+    DeviceGuard keep(-1);  // (the shards' buffers are freed on this thread, each on its device)
+    try {
+        const std::vector<uint64_t> first = shard_bounds(in_off, count, (int)devs.size());
+        std::vector<std::unique_ptr<Shard>> sh;
+        for (size_t k = 0; k < devs.size(); k++) {
+            sh.emplace_back(new Shard());
+            sh[k]->dev = devs[k];
+            sh[k]->first = first[k];
+            sh[k]->count = first[k + 1] - first[k];
+        }
+        // phase 1: per shard, upload, K1 into bound-sized slots, K3 into a packed shard; its sizes back
+        e = each_shard(sh, [&](Shard &x) -> int {
+            const uint64_t c = x.count, base = in_off[x.first], nb = in_off[x.first + c] - base;
+            std::vector<uint64_t> ioff(c + 1), ooff(c + 1);
+            uint64_t mx = 0;
+            ooff[0] = 0;
+            for (uint64_t t = 0; t <= c; t++) ioff[t] = in_off[x.first + t] - base;
+            for (uint64_t t = 0; t < c; t++) {
+                const uint64_t n = ioff[t + 1] - ioff[t];
+                mx = n > mx ? n : mx;
+                ooff[t + 1] = ooff[t] + ((ez_compress_bound(n) + 15) & ~15ull);
+            }
+            if (x.in.ensure(nb + 64) || x.in_off.ensure(8 * (c + 1)) || x.out.ensure(ooff[c] + 64) || x.out_off.ensure(8 * (c + 1)) ||
+                x.size.ensure(8 * c) || x.status.ensure(4 * c) || x.ws.ensure(ez_pack_workspace(c) + 64) || x.packed.ensure(ooff[c] + 64) ||
+                x.packed_off.ensure(8 * (c + 1)))
+                return EZ_EDEVICE;
+            if (nb) EZ_SHARD_HIP(hipMemcpyAsync(x.in.p, in + base, nb, hipMemcpyHostToDevice, x.st));
+            EZ_SHARD_HIP(hipMemcpyAsync(x.in_off.p, ioff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.st));
+            EZ_SHARD_HIP(hipMemcpyAsync(x.out_off.p, ooff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.st));
+            ez_batch b{x.in.as<uint8_t>(), x.in_off.as<uint64_t>(), x.out.as<uint8_t>(), x.out_off.as<uint64_t>(),
+                       x.size.as<uint64_t>(), x.status.as<int32_t>(), c, mx};
+            int r = ez_compress_batch(block, htable, flags, &b, x.st);
+            if (r != EZ_OK) return r;
+            r = ez_pack_batch(x.out.as<uint8_t>(), x.out_off.as<uint64_t>(), x.size.as<uint64_t>(), c, x.packed.as<uint8_t>(),
+                              x.packed_off.as<uint64_t>(), x.ws.p, x.st);
+            if (r != EZ_OK) return r;
+            // the shard's packed offsets straight into the caller's array (rebased below; its last one,
+            // the shard's total, is the next shard's first entry and comes back separately)
+            EZ_SHARD_HIP(hipMemcpyAsync(packed_off + x.first, x.packed_off.p, 8 * c, hipMemcpyDeviceToHost, x.st));
+            EZ_SHARD_HIP(hipMemcpyAsync(&x.total, x.packed_off.as<uint64_t>() + c, 8, hipMemcpyDeviceToHost, x.st));
+            if (status) EZ_SHARD_HIP(hipMemcpyAsync(status + x.first, x.status.p, 4 * c, hipMemcpyDeviceToHost, x.st));
+            EZ_SHARD_HIP(hipStreamSynchronize(x.st));
+            return EZ_OK;
+        });
+        if (e != EZ_OK) return e;
+        // the global packing: shard k starts where shard k-1 ends (a host exclusive scan of the totals)
+        uint64_t at = 0;
+        for (auto &x : sh) {
+            x->base = at;
+            at += x->total;
+            for (uint64_t t = 0; t < x->count; t++) packed_off[x->first + t] += x->base;
+        }
+        packed_off[count] = at;
+        if (at > packed_cap) return EZ_ENOSPC;
+        // phase 2: every shard's packed bytes down to its place
+        return each_shard(sh, [&](Shard &x) -> int {
+            if (x.total) EZ_SHARD_HIP(hipMemcpyAsync(packed + x.base, x.packed.p, x.total, hipMemcpyDeviceToHost, x.st));
+            EZ_SHARD_HIP(hipStreamSynchronize(x.st));
+            return EZ_OK;
+        });
+    } catch (...) {
+        return EZ_EDEVICE;  // (host allocation failure: nothing unwinds across the C-ABI)
+    }
+}
+
+extern "C" int ez_decompress_batch_multi(int64_t block_size_limit, const uint8_t *in, const uint64_t *in_off, uint64_t count,
+                                         const int *devices, int ndev, uint8_t *out, const uint64_t *out_off, uint64_t *out_size,
+                                         int32_t *status) {
+    if (!in_off || !out_off || !out_size) return EZ_EINVAL;
+    std::vector<int> devs;
+    int e = resolve_devices(devices, ndev, devs);
+    if (e != EZ_OK) return e;
+    if (count == 0) return EZ_OK;
+    DeviceGuard keep(-1);
+    try {
+        const std::vector<uint64_t> first = shard_bounds(in_off, count, (int)devs.size());
+        std::vector<std::unique_ptr<Shard>> sh;
+        for (size_t k = 0; k < devs.size(); k++) {
+            sh.emplace_back(new Shard());
+            sh[k]->dev = devs[k];
+            sh[k]->first = first[k];
+            sh[k]->count = first[k + 1] - first[k];
+        }
+        return each_shard(sh, [&](Shard &x) -> int {
+            const uint64_t c = x.count, ib = in_off[x.first], nb = in_off[x.first + c] - ib;
+            const uint64_t ob = out_off[x.first], no = out_off[x.first + c] - ob;
+            std::vector<uint64_t> ioff(c + 1), ooff(c + 1);
+            uint64_t mx = 0;
+            for (uint64_t t = 0; t <= c; t++) {
+                ioff[t] = in_off[x.first + t] - ib;
+                ooff[t] = out_off[x.first + t] - ob;
+                if (t) mx = ooff[t] - ooff[t - 1] > mx ? ooff[t] - ooff[t - 1] : mx;
+            }
+            if (x.in.ensure(nb + 64) || x.in_off.ensure(8 * (c + 1)) || x.out.ensure(no + 64) || x.out_off.ensure(8 * (c + 1)) ||
+                x.size.ensure(8 * c) || x.status.ensure(4 * c) || x.ws.ensure(ez_decompress_workspace(c) + 64))
+                return EZ_EDEVICE;
+            if (nb) EZ_SHARD_HIP(hipMemcpyAsync(x.in.p, in + ib, nb, hipMemcpyHostToDevice, x.st));
+            EZ_SHARD_HIP(hipMemcpyAsync(x.in_off.p, ioff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.st));
+            EZ_SHARD_HIP(hipMemcpyAsync(x.out_off.p, ooff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.st));
+            // (the largest slot given: the decoder route needs no device read-back)
+            ez_batch b{x.in.as<uint8_t>(), x.in_off.as<uint64_t>(), x.out.as<uint8_t>(), x.out_off.as<uint64_t>(),
+                       x.size.as<uint64_t>(), x.status.as<int32_t>(), c, mx ? mx : 1};
+            const int r = ez_decompress_batch(block_size_limit, &b, x.ws.p, x.st);
+            if (r != EZ_OK) return r;
+            if (no) EZ_SHARD_HIP(hipMemcpyAsync(out + ob, x.out.p, no, hipMemcpyDeviceToHost, x.st));
+            EZ_SHARD_HIP(hipMemcpyAsync(out_size + x.first, x.size.p, 8 * c, hipMemcpyDeviceToHost, x.st));
+            if (status) EZ_SHARD_HIP(hipMemcpyAsync(status + x.first, x.status.p, 4 * c, hipMemcpyDeviceToHost, x.st));
+            EZ_SHARD_HIP(hipStreamSynchronize(x.st));
+            return EZ_OK;
+        });
+    } catch (...) {
+        return EZ_EDEVICE;
+    }
 }

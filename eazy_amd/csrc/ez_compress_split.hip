@@ -575,9 +575,12 @@ struct WinRoll {
     }
 };
 
-// WinRoll with the current region in LDS (LW, experiments): the group's 144-byte buffer holds stream
-// bytes [cb, cb + 128); a window's 32 bytes are nine aligned dword reads and eight v_alignbyte, instead
-// of ten ds_bpermute, nine selects and eight v_alignbyte from the lanes' registers
+// WinRoll with the current region in LDS (LW): the group's 144-byte buffer holds stream bytes
+// [cb, cb + 128); a window's 32 bytes are nine aligned dword reads and eight v_alignbyte, instead
+// of ten ds_bpermute, nine selects and eight v_alignbyte from the lanes' registers.  R: the
+// farthest window start the region serves (80 for 32-byte windows; 64 for the 48-byte windows of
+// the 40-byte judgement, whose bytes reach i + 15 + 39)
+template <int R = 80>
 struct WinLds {
     uint32_t f0, f1;  // this lane's dwords of the prefetched region
     int32_t cb, fb, bmax, pm;
@@ -605,8 +608,8 @@ struct WinLds {
     }
     __device__ __forceinline__ void advance(const uint8_t *p, int32_t i, int lj, bool live) {
         const int32_t y = i - 8;
-        if (live && !(y >= cb && y - cb <= 80)) {
-            if (!(y >= fb && y - fb <= 80)) {
+        if (live && !(y >= cb && y - cb <= R)) {
+            if (!(y >= fb && y - fb <= R)) {
                 fb = min(floor4(y), bmax);
                 ld(p, fb, lj, f0, f1);
             }
@@ -629,6 +632,21 @@ struct WinLds {
         w0.hi = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
         w1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
         w1.hi = (uint64_t)b[6] | ((uint64_t)b[7] << 32);
+    }
+    // x-8 .. x+39 (R = 64: o <= 79, the reads end at byte 131 of the 144-byte buffer)
+    __device__ __forceinline__ void bytes48(int32_t i, int g, int lj, V16 &w0, V16 &w1, V16 &w2) const {
+        static_assert(R <= 64, "48-byte windows need the region to reach i + 54");
+        const uint32_t o = (uint32_t)(i - 8 - cb + lj), r = o & 3;
+        const uint32_t *q = (const uint32_t *)(wl + (o & ~3u));
+        uint32_t d[13];
+#pragma unroll
+        for (int t = 0; t < 13; t++) d[t] = q[t];
+        uint32_t b[12];
+#pragma unroll
+        for (int t = 0; t < 12; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+        w0 = V16{(uint64_t)b[0] | ((uint64_t)b[1] << 32), (uint64_t)b[2] | ((uint64_t)b[3] << 32)};
+        w1 = V16{(uint64_t)b[4] | ((uint64_t)b[5] << 32), (uint64_t)b[6] | ((uint64_t)b[7] << 32)};
+        w2 = V16{(uint64_t)b[8] | ((uint64_t)b[9] << 32), (uint64_t)b[10] | ((uint64_t)b[11] << 32)};
     }
 };
 constexpr int32_t kWinLdsBytes = 144;
@@ -674,6 +692,23 @@ __device__ __forceinline__ void bytes32(const LeanIn &L, const uint8_t *p, int32
     c0.hi = (uint64_t)b[2] | ((uint64_t)b[3] << 32);
     c1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
     c1.hi = (uint64_t)b[6] | ((uint64_t)b[7] << 32);
+}
+
+// y-8 .. y+39 (the 40-byte judgement): dwordx4 x3 + dword from floor4(p + y - 8), unchecked (padded
+// streams: k1_lean's edge slots leave 64 readable bytes after every stream)
+__device__ __forceinline__ void bytes48(const LeanIn &L, const uint8_t *p, int32_t y, V16 &c0, V16 &c1, V16 &c2) {
+    const uintptr_t a = (uintptr_t)(p + y - 8);
+    const uint32_t r = (uint32_t)(a & 3);
+    const uint8_t *w = (const uint8_t *)(a & ~(uintptr_t)3);
+    const uint4 q0 = L.dw4(w), q1 = L.dw4(w + 16), q2 = L.dw4(w + 32);
+    const uint32_t q3 = L.dw(w + 48);
+    const uint32_t d[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3};
+    uint32_t b[12];
+#pragma unroll
+    for (int t = 0; t < 12; t++) b[t] = __builtin_amdgcn_alignbyte(d[t + 1], d[t], r);
+    c0 = V16{(uint64_t)b[0] | ((uint64_t)b[1] << 32), (uint64_t)b[2] | ((uint64_t)b[3] << 32)};
+    c1 = V16{(uint64_t)b[4] | ((uint64_t)b[5] << 32), (uint64_t)b[6] | ((uint64_t)b[7] << 32)};
+    c2 = V16{(uint64_t)b[8] | ((uint64_t)b[9] << 32), (uint64_t)b[10] | ((uint64_t)b[11] << 32)};
 }
 
 // Byte counts without branches: v_ffbl / v_ffbh return ~0u for 0, and saturating adds keep that
@@ -771,31 +806,110 @@ __device__ __forceinline__ void lds_put12(uint64_t *tab, uint32_t h, uint32_t va
     asm volatile("ds_mskor_b64 %0, %1, %2" : : "v"(addr), "v"(m), "v"(v) : "memory");
 }
 
+constexpr int kEdgeSlots = 40;
+constexpr int32_t kEdgeBefore = 64;  // readable bytes before a stream (WinRoll's regions), 64 after it
+__host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + kEdgeBefore + 64 + 15) & ~15ull; }
+__host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs &a) { return 128 + kEdgeSlots * edge_slot_bytes(a) + 16; }
+
+// k1_lean's parse of fresh single-Write streams, 16 lanes (a group) per stream, 4 groups per wave.
 // TB: the table's visit -- 0 the DPP search over a u16 table, 16 lds_mskor16, 12 lds_mskor12;
-// NT: the records are stored nontemporal (read back by another kernel) or plain (by this wave)
-template <int TB, bool NT = true, bool LW = false>
-__device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int32_t n, int lj, int g, uint16_t *hth,
-                                          uint32_t hsh, uint64_t *recw, uint32_t roff, uint64_t rcap, int prio, int32_t &nrec_out,
-                                          int &err, uint8_t *wl = nullptr) {
-    // (the records at recw + roff: recw is the wave's, in scalar registers, roff the group's)
-    constexpr int G = 16;
-    int32_t i = 0, done = 0, nrec = 0;
-    bool live = !err && n >= 4;
-    int32_t guard = 4 * n + 64;
-    V16 w0{0, 0}, w1{0, 0};  // bytes x-8 .. x+7 and x+8 .. x+23 of this lane's position x
-    typename std::conditional<LW, WinLds, WinRoll>::type wr;
+// LW: the window's region in LDS (WinLds) or in the lanes' registers (WinRoll);
+// FW: the judgement's forward cap, 24 or 40 bytes (40: 48-byte windows and candidates, LW only);
+// PERSIST: a group whose stream ends takes the next one from the batch's queue (a global counter)
+// instead of idling until the wave's other three groups end theirs; the grid is then the resident
+// waves of the chip, and a wave ends when the queue is empty and its groups are done.
+template <int TB, bool LW, int FW, bool PERSIST>
+__device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, uint16_t *hth, uint32_t table_words, uint32_t hsh,
+                                         uint64_t *recs, uint64_t rcap, int prio, uint8_t *edge, uint8_t *wl) {
+    constexpr int G = 16, S = 64 / G;
+    constexpr bool W40 = FW == 40;
+    static_assert(FW == 24 || (W40 && LW), "the 40-byte judgement reads its windows from the LDS region");
+    constexpr int32_t CAP = W40 ? 40 : kFwdCap;
+    const LeanIn L{};
+    const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
+    uint32_t *queue = (uint32_t *)(edge + 128 + kEdgeSlots * edge_slot_bytes(A)) + 1;  // [0]: edge slots taken
+    const uint32_t rcap32 = (uint32_t)rcap;
+
+    // the group's stream: index, bytes, size, error, record base; its parse state
+    uint64_t s = (uint64_t)blockIdx.x * S + (uint64_t)g;
+    const uint8_t *p = edge + 16;
+    int32_t n = 0, i = 0, done = 0, nrec = 0;
+    int err = 0;
+    bool live = false, pending = false;
+    uint64_t *rec = recs;
+    typename std::conditional<LW, WinLds<W40 ? 64 : 80>, WinRoll>::type wr;
     if constexpr (LW) wr.wl = wl;
-    wr.init(p, n, lj, live);
-    // the bytes around stream position 0, the candidate of every zero table entry:
-    // judged without a load
-    V16 z0{0, 0}, z1{0, 0};
-    if (live) {
-        bytes32(L, p, 0, z0, z1);
-        z0.lo = 0;
-    }
-    while (__ballot(live) != 0) {
-        wr.bytes(i, g, lj, w0, w1);
-        if (live && --guard < 0) { err = EZ_ESTUCK; live = false; }
+    // iterations left to the wave (SALU): every stream opened adds its parse's bound, so a correct
+    // parse never reaches 0 and a wrong one cannot hang the grid
+    int64_t budget = 0;
+
+    // open stream s for the group (group-uniform, in a branch of the group's lanes): table zeroed,
+    // edge streams copied into a padded slot, the first region of the window loaded
+    auto open = [&]() {
+        pending = s < A.count;
+        n = 0;
+        const uint8_t *src = blo;
+        if (pending) {
+            n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+            src = A.in + A.in_off[s];
+        }
+        for (int32_t k = 4 * lj; k < (int32_t)table_words; k += 4 * G) *(uint4 *)((uint32_t *)hth + k) = make_uint4(0, 0, 0, 0);
+        // the launcher sized records and tables from max_len: longer streams are refused
+        err = !pending || (uint64_t)n > A.max_len ? EZ_EINVAL : 0;
+        live = !err && n >= 4;
+        p = live ? src : edge + 16;
+        const bool edge_stream = live && (src - kEdgeBefore < blo || src + n + 64 > bhi);
+        if (edge_stream) {
+            // [64 zero bytes][the stream][64 zero bytes]
+            int32_t slot = 0;
+            if (lj == 0) slot = (int32_t)atomicAdd(queue - 1, 1u);
+            slot = bcast(slot, G * g);
+            if (slot >= kEdgeSlots) {  // cannot happen (the batch has at most two edge regions)
+                err = EZ_ESTUCK;
+                live = false;
+                p = edge + 16;
+            } else {
+                uint8_t *d = edge + 128 + (uint64_t)slot * edge_slot_bytes(A);
+                for (int32_t k = lj; k < n + kEdgeBefore + 64; k += G)
+                    d[k] = (k >= kEdgeBefore && k < n + kEdgeBefore) ? src[k - kEdgeBefore] : (uint8_t)0;
+                p = d + kEdgeBefore;
+            }
+            __threadfence_block();
+        }
+        i = done = nrec = 0;
+        rec = recs + (pending ? s : 0) * rcap;
+        wr.init(p, n, lj, live);
+    };
+    open();
+    budget += (int64_t)(4 * A.max_len + 64) * S;
+
+    V16 w0{0, 0}, w1{0, 0}, w2{0, 0};  // bytes x-8 .. x+7, x+8 .. x+23 (and x+24 .. x+39) of this lane's x
+    for (;;) {
+        // groups whose stream ended: its size word, then (PERSIST) the next stream
+        if (__ballot(!live && pending) != 0) {
+            if (!live && pending) {
+                if (lj == 0) A.out_size[s] = (uint64_t)((EZ_EXP & 32768) ? 0 : nrec) | ((uint64_t)err << 48);
+                pending = false;
+                if (PERSIST) {
+                    uint32_t q = 0;
+                    if (lj == 0) q = atomicAdd(queue, 1u);
+                    s = (uint64_t)gridDim.x * S + (uint64_t)(uint32_t)bcast((int32_t)q, G * g);
+                    open();
+                }
+            }
+            if (PERSIST) budget += (int64_t)(4 * A.max_len + 64) * (__builtin_popcountll(__ballot(pending)) / G);
+        }
+        if (__ballot(live) == 0) {
+            if (PERSIST && __ballot(pending) != 0) continue;
+            break;
+        }
+        if (--budget < 0) {
+            if (live) err = EZ_ESTUCK;
+            live = false;
+            continue;
+        }
+        if constexpr (W40) wr.bytes48(i, g, lj, w0, w1, w2);
+        else wr.bytes(i, g, lj, w0, w1);
         const int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
         const int32_t x = i + lj;
         const bool valid = live && lj < nvalid;
@@ -813,19 +927,21 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
             const int32_t d = PredZ<G - 1>::get(valid ? h + 1 : 0u, 0);
             cand = valid ? (d ? x - d : tv) : 0;
         }
-        V16 c0 = z0, c1 = z1;
-        if (cand != 0) {
-            if (kFwdCap == 20) bytes28(L, p, cand, c0, c1);
-            else bytes32(L, p, cand, c0, c1);
-            // bytes before the stream start are the fresh ring's zeros (rare: a branch)
-            if (__builtin_expect(cand < 8, 0)) c0.lo &= ~0ull << (8 * (8 - cand));
-        }
+        // the candidate's bytes, every lane (a zero table entry is stream position 0, SURVEY A.2:
+        // its bytes load like any other; the 64 bytes before a stream are readable)
+        V16 c0, c1, c2{0, 0};
+        if constexpr (W40) bytes48(L, p, cand, c0, c1, c2);
+        else if (kFwdCap == 20) bytes28(L, p, cand, c0, c1);
+        else bytes32(L, p, cand, c0, c1);
+        // bytes before the stream start are the fresh ring's zeros (rare: a branch)
+        if (__builtin_expect(cand < 8, 0)) c0.lo = cand == 0 ? 0ull : c0.lo & (~0ull << (8 * (8 - cand)));
         if (prio & 1) __builtin_amdgcn_s_setprio(0);
 
         // ---- capped judgement, writer.go:219-301 (window) and :441-463 (writeRunlen)
         const bool rl = cand >= done && cand < x;
         const uint64_t e0 = w0.hi ^ c0.hi, e1 = w1.lo ^ c1.lo, e2 = w1.hi ^ c1.hi;
-        int32_t jf = kFwdCap == 20 ? first_diff20(e0, e1, (uint32_t)e2) : first_diff24(e0, e1, e2);
+        int32_t jf = W40 ? first_diff40(e0, e1, e2, w2.lo ^ c2.lo, w2.hi ^ c2.hi)
+                         : (kFwdCap == 20 ? first_diff20(e0, e1, (uint32_t)e2) : first_diff24(e0, e1, e2));
         jf = jf < n - x ? jf : n - x;
         int32_t bl = x - done;
         if (rl) bl = bl < cand ? bl : cand;
@@ -839,28 +955,28 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         int32_t lit, nx, dist, ext;
         bool force = false;
         if (zr) {  // writeZeros :407-439
-            int32_t zf = kFwdCap == 20 ? first_diff20(0, c1.lo, (uint32_t)c1.hi) : first_diff24(0, c1.lo, c1.hi);
+            int32_t zf = W40 ? first_diff40(0, c1.lo, c1.hi, c2.lo, c2.hi)
+                             : (kFwdCap == 20 ? first_diff20(0, c1.lo, (uint32_t)c1.hi) : first_diff24(0, c1.lo, c1.hi));
             zf = zf < n - cand ? zf : n - cand;
             int32_t zb = last_diff8(c0.lo);
             zb = zb < cand - done ? zb : cand - done;
             lit = cand - zb;
             nx = cand + zf;
             dist = 0;
-            ext = (zf == kFwdCap && n - cand > kFwdCap ? 1 : 0) | (zb == 8 && cand - done > 8 ? 2 : 0);
+            ext = (zf == CAP && n - cand > CAP ? 1 : 0) | (zb == 8 && cand - done > 8 ? 2 : 0);
         } else {  // writeRunlen :441-489 / window match :303-321
             lit = x - jb;
             nx = x + fw;
             dist = x - cand;
             force = rl;
-            ext = (jf == kFwdCap && (rl ? n - x : (done - cand < n - x ? done - cand : n - x)) > kFwdCap ? 1 : 0) |
+            ext = (jf == CAP && (rl ? n - x : (done - cand < n - x ? done - cand : n - x)) > CAP ? 1 : 0) |
                   (jb == 8 && bl > 8 ? 2 : 0);
         }
         const uint64_t am64 = __ballot(acc);
         const uint32_t am = (uint32_t)(am64 >> (G * g)) & 0xffffu;
         const int a = am ? __builtin_ctz(am) : -1;
         const bool act = live && a >= 0;
-        // the group's next position (and whether the acceptor needs an exact extension), one
-        // v_readlane per group
+        // the group's next position (and whether the acceptor needs an exact extension)
         const int32_t pack = nx | (ext << 28);
         // (one ds_bpermute from each group's first acceptor: fewer VALU than four v_readlane + selects)
         const int32_t sel = __builtin_amdgcn_ds_bpermute(4 * (G * g + (a < 0 ? 0 : a)), pack);
@@ -880,7 +996,7 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
             const int32_t blim = zra ? ca - done : (rla ? ((xa - done) < ca ? (xa - done) : ca) : xa - done);
             const int32_t flim = zra ? n - ca : (rla ? n - xa : ((done - ca) < n - xa ? done - ca : n - xa));
             int32_t fx, cx;
-            gext<G, GWU>(GWU{p}, need && (e & 1), need && (e & 2), g, lj, fa, ca, mode, done, kFwdCap, flim, blim, fx, cx);
+            gext<G, GWU>(GWU{p}, need && (e & 1), need && (e & 2), g, lj, fa, ca, mode, done, CAP, flim, blim, fx, cx);
             if (need) {
                 const int32_t f = (e & 1) ? fx : (sel & 0x0fffffff) - fa;
                 const int32_t c = (e & 2) ? cx : ((ib >> 16) & 0xf);
@@ -909,11 +1025,11 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         // the record, stored after the next region's load is issued (a region switch waits for every
         // vector-memory operation before it, stores included)
         const bool st_rec = act && lj == a;
-        const uint64_t rec = rec_pack(lit, nx - lit, dist, force);
-        const uint32_t rat = roff + (uint32_t)nrec;
-        const bool rec_room = (uint64_t)nrec < rcap;
+        const uint64_t rv = rec_pack(lit, nx - lit, dist, force);
+        const uint32_t rat = (uint32_t)nrec;
+        const bool rec_room = (uint32_t)nrec < rcap32;
         if (act) {
-            if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
+            if (!rec_room) { err = EZ_ESTUCK; live = false; }
             nrec++;
             i = done = nxt;
         } else if (live) {
@@ -924,16 +1040,12 @@ __device__ __forceinline__ void lean_loop(const LeanIn &L, const uint8_t *p, int
         __builtin_amdgcn_sched_barrier(0);
         if (st_rec) {
 #if !(EZ_EXP & 32768)
-            if (rec_room) {
-                if (NT) __builtin_nontemporal_store(rec, recw + rat);
-                else recw[rat] = rec;
-            }
+            if (rec_room) __builtin_nontemporal_store(rv, rec + rat);
 #else  // (timing builds: the records' traffic without their lines -- k1_emit then sees none)
-            __builtin_nontemporal_store(rec, recw + (roff + (uint32_t)(nrec & 1)));
+            __builtin_nontemporal_store(rv, rec + (uint32_t)(nrec & 1));
 #endif
         }
     }
-    nrec_out = nrec;
 }
 
 // ---------------------------------------------------------------- K1L: long fresh streams
@@ -1557,18 +1669,11 @@ __global__ __launch_bounds__(256) void k1_ring_store(CompressArgs A) {
 // launcher).  A live stream (n >= 4) lacks the 64 bytes before or the 64 after it only if it starts
 // in the batch's first 64 bytes (at most 16 such streams, each >= 4 bytes) or ends in its last 64
 // (at most 16): 32 slots always suffice.
-constexpr int kEdgeSlots = 40;
-constexpr int32_t kEdgeBefore = 64;  // readable bytes before a stream (WinRoll's regions), 64 after it
-__host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + kEdgeBefore + 64 + 15) & ~15ull; }
-__host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs &a) { return 128 + kEdgeSlots * edge_slot_bytes(a) + 16; }
-
 template <bool WIDE>
 __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
                                             uint64_t *stage = nullptr);
 
-// FUSE: the wave writes its four streams' tokens itself after the parse (emit_stream, one stream at a
-// time by the whole wave), instead of a separate k1_emit launch reading the records back
-template <int TB, bool FUSE = false, bool LW = false>
+template <int TB, bool LW = false, int FW = 24, bool PERSIST = false>
 __global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                  uint64_t rcap, int prio, uint8_t *edge) {
     constexpr int G = 16, S = 64 / G;
@@ -1578,56 +1683,9 @@ __global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, 
     const int32_t hs = (int32_t)A.hs;
     const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(hs - 1)));
     uint16_t *hth = (uint16_t *)((uint32_t *)smem + (uint32_t)g * stride_words);
-    const uint64_t s = (uint64_t)blockIdx.x * S + g;
-    const bool have = s < A.count;
-    const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
-    int32_t n = 0;
-    const uint8_t *src = blo;
-    if (have) {
-        n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
-        src = A.in + A.in_off[s];
-    }
-    for (int32_t k = 4 * lj; k < (int32_t)table_words; k += 4 * G) *(uint4 *)((uint32_t *)hth + k) = make_uint4(0, 0, 0, 0);
-    // the launcher sized records and tables from max_len: longer streams are refused; a lane
-    // group without a live stream never enters the loop and reads only the dummy region
-    int err = !have || (uint64_t)n > A.max_len ? EZ_EINVAL : 0;
-    const bool live = !err && n >= 4;
-    uint64_t *recw = recs + (uint64_t)blockIdx.x * S * rcap;  // (the wave's records; group g's at g * rcap)
-    const uint32_t roff = (uint32_t)(g * rcap);
-    const uint8_t *p = live ? src : edge + 16;
-    const bool edge_stream = live && (src - kEdgeBefore < blo || src + n + 64 > bhi);
-    if (__ballot(edge_stream) != 0) {
-        // copy each edge stream of the wave into a slot: [64 zero bytes][the stream][64 zero bytes]
-        int32_t slot = 0;
-        if (edge_stream && lj == 0) slot = (int32_t)atomicAdd((uint32_t *)(edge + 128 + kEdgeSlots * edge_slot_bytes(A)), 1u);
-        slot = bcast(slot, G * g);
-        if (edge_stream && slot >= kEdgeSlots) {  // cannot happen (32 slots suffice)
-            err = EZ_ESTUCK;
-            p = edge + 16;
-        }
-        if (edge_stream && !err) {
-            uint8_t *d = edge + 128 + (uint64_t)slot * edge_slot_bytes(A);
-            for (int32_t k = lj; k < n + kEdgeBefore + 64; k += G)
-                d[k] = (k >= kEdgeBefore && k < n + kEdgeBefore) ? src[k - kEdgeBefore] : (uint8_t)0;
-            p = d + kEdgeBefore;
-        }
-        __threadfence_block();
-    }
-    int32_t nrec = 0;
     // (LW: the groups' window buffers after the four tables)
     uint8_t *wl = smem + (size_t)4 * stride_words * S + (size_t)g * kWinLdsBytes;
-    lean_loop<TB, !FUSE, LW>(LeanIn{}, p, n, lj, g, hth, hsh, recw, roff, rcap, prio, nrec, err, wl);
-    if (have && lj == 0) A.out_size[s] = (uint64_t)((EZ_EXP & 32768) ? 0 : nrec) | ((uint64_t)err << 48);
-    if (FUSE) {
-        // the records and counts this wave stored, visible to all its lanes (one wave, one CU: its
-        // stores complete, then its loads read them through the same L1)
-        __builtin_amdgcn_s_waitcnt(0);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
-        for (int q = 0; q < S; q++) {
-            const uint64_t sq = (uint64_t)blockIdx.x * S + (uint64_t)q;
-            if (sq < A.count) emit_stream<false>(A, recs, rcap, sq, lane);
-        }
-    }
+    lean_run<TB, LW, FW, PERSIST>(A, lj, g, hth, table_words, hsh, recs, rcap, prio, edge, wl);
 }
 
 // ---------------------------------------------------------------- K1e
@@ -1868,14 +1926,43 @@ bool split_lean() {
     static const bool v = knob("EZ_K1S_LEAN", 1) != 0;
     return v;
 }
-hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
+// resident blocks of a k1_lean variant on the device (per process; the persistent grid)
+template <int TB, bool LW, int FW, bool PERSIST>
+unsigned lean_resident(size_t lds) {
+    static unsigned cached = 0;
+    static size_t cached_lds = 0;
+    if (cached == 0 || cached_lds != lds) {
+        int dev = 0, cus = 0, per = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k1_lean<TB, LW, FW, PERSIST>, 64, lds) != hipSuccess || per <= 0 ||
+            cus <= 0)
+            return 0;
+        cached = (unsigned)(per * cus);
+        cached_lds = lds;
+    }
+    return cached;
+}
+
+template <int TB, bool LW, int FW>
+hipError_t launch_lean_v(const CompressArgs &a, uint64_t *recs, uint32_t stride, uint32_t tw, size_t lds, int prio, uint8_t *edge,
+                         bool persist, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_lean<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void *)k1_lean<16>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void *)k1_lean<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<TB, LW, FW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<TB, LW, FW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
+    const uint64_t rcap = rec_cap(a);
+    const uint64_t blocks = (a.count + 3) / 4;
+    const unsigned res = persist ? lean_resident<TB, LW, FW, true>(lds) : 0;
+    if (res != 0 && blocks > res)
+        hipLaunchKernelGGL((k1_lean<TB, LW, FW, true>), dim3(res), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
+    else
+        hipLaunchKernelGGL((k1_lean<TB, LW, FW, false>), dim3((unsigned)blocks), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
+    return hipGetLastError();
+}
+
+hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     // the visit by one ds_mskor (when its lane order holds); EZ_K1S_MSK=0 takes the DPP search (A/B).
     // EZ_K1S_T12=1 (A/B) puts streams of <= 4099 bytes on 12-bit tables: 6 waves per SIMD instead of
     // 5 measured the same at C1 (k1_lean 2,100 against 2,095 us), so the u16 tables stay
@@ -1886,44 +1973,34 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     const uint32_t w12 = (uint32_t)((2 * ((a.hs + 4) / 5) + 3) & ~3ll);  // u32 words of a 12-bit table
     const uint32_t stride = t12 ? w12 : split_stride<16, true>(a), tw = t12 ? w12 : split_table_words<true>(a);
     const uint64_t rcap = rec_cap(a);
-    const unsigned grid = (unsigned)((a.count + S - 1) / S);
     static const int prio = knob("EZ_K1S_PRIO", 1);
     uint8_t *edge = (uint8_t *)(recs + a.count * rcap);
+    // (the edge area's first 128 bytes: the dummy region of idle groups; its last 16: the edge-slot
+    // counter and the stream queue)
     hipError_t z = hipMemsetAsync(edge, 0, 128, st);
     if (z == hipSuccess) z = hipMemsetAsync(edge + 128 + kEdgeSlots * edge_slot_bytes(a), 0, 16, st);
     if (z != hipSuccess) return z;
     // EZ_K1S_LDSPAD (experiments): extra LDS per block, to cap the streams resident per CU
     static const size_t pad = (size_t)knob("EZ_K1S_LDSPAD", 0);
-    // EZ_K1S_FUSE=1 (A/B): the token writer inside the parse kernel
-    static const bool fuse = knob("EZ_K1S_FUSE", 0) != 0;
-    if (fuse && msk && !t12) {
-        static bool fattr = false;
-        if (!fattr) {
-            (void)hipFuncSetAttribute((const void *)k1_lean<16, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            fattr = true;
-        }
-        hipLaunchKernelGGL((k1_lean<16, true>), dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
-        return hipGetLastError();
-    }
     // the window's region in LDS (WinLds; C1 K1 2.18 -> 2.08 ms, A/B on one box); EZ_K1S_LW=0 (A/B) keeps it in the lanes' registers
     static const bool lw = knob("EZ_K1S_LW", 1) != 0;
+    // the judgement's forward cap: 40 bytes (48-byte windows and candidates; C1 K1 2.081 -> 2.012 ms,
+    // A/B on one box) or 24; EZ_K1S_FW=24 (A/B)
+    static const bool w40 = knob("EZ_K1S_FW", 40) == 40;
+    // persistent groups (a stream queue); EZ_K1S_PERSIST=0 (A/B): one launch block per 4 streams
+    static const bool persist = knob("EZ_K1S_PERSIST", 1) != 0;
+    const size_t lds = (size_t)stride * 4 * S + (lw && msk ? (size_t)kWinLdsBytes * S : 0) + pad;
+    hipError_t e;
     if (lw && msk) {
-        static bool lattr = false;
-        if (!lattr) {
-            (void)hipFuncSetAttribute((const void *)k1_lean<12, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            (void)hipFuncSetAttribute((const void *)k1_lean<16, false, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-            lattr = true;
-        }
-        const size_t lds = (size_t)stride * 4 * S + (size_t)kWinLdsBytes * S + pad;
-        if (t12) hipLaunchKernelGGL((k1_lean<12, false, true>), dim3(grid), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
-        else hipLaunchKernelGGL((k1_lean<16, false, true>), dim3(grid), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
+        if (t12) e = launch_lean_v<12, true, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
+        else if (w40) e = launch_lean_v<16, true, 40>(a, recs, stride, tw, lds, prio, edge, persist, st);
+        else e = launch_lean_v<16, true, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
     } else if (t12)
-        hipLaunchKernelGGL(k1_lean<12>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
+        e = launch_lean_v<12, false, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
     else if (msk)
-        hipLaunchKernelGGL(k1_lean<16>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
+        e = launch_lean_v<16, false, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
     else
-        hipLaunchKernelGGL(k1_lean<0>, dim3(grid), dim3(64), (size_t)stride * 4 * S + pad, st, a, stride, tw, recs, rcap, prio, edge);
-    hipError_t e = hipGetLastError();
+        e = launch_lean_v<0, false, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
     if (e != hipSuccess) return e;
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
     hipLaunchKernelGGL(k1_emit<false>, dim3(egrid), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);

@@ -212,6 +212,16 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
         d.blk = out;
         int64_t i = 0, total = 0;
         int err = EZ_OK;
+        // (a stream a fast decoder handed over is recomputed from its start: so are its breaks)
+        if (A.breaks && lane == 0) A.breaks[0] = 0;
+        // K2t found the slot too small (a caller sizing its slot, end_state[0] = -2): no re-decode
+        if (A.end_state && A.end_state[0] == -2) {
+            if (lane == 0) {
+                A.out_size[s] = 0;
+                if (A.status) A.status[s] = EZ_ENOSPC;
+            }
+            continue;
+        }
         for (int64_t guard = 0;; guard++) {
             if (guard > d.nb + 64) { err = EZ_ESTUCK; break; }
             const int64_t left = cap - total;
@@ -223,7 +233,10 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
                 if (m > 0) { err = EZ_ENOSPC; break; }
             }
             total += m;
-            if (err == EZ_EBREAK && A.breaks && lane == 0) atomicAdd(A.breaks, 1u);
+            if (err == EZ_EBREAK && A.breaks && lane == 0) {
+                const uint64_t at = A.breaks[0]++;
+                if (at < A.breaks_cap) A.breaks[1 + at] = (uint64_t)total;
+            }
             if (err == EZ_OK || err == EZ_EBREAK) continue;
             if (err == EZ_ESHORTBUF) err = (d.state != 0 || i < d.nb) ? EZ_EUNEXPECTEDEOF : EZ_OK;
             break;
@@ -231,27 +244,27 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
         if (lane == 0) {
             A.out_size[s] = (uint64_t)total;
             if (A.status) A.status[s] = err;
+            if (A.end_state) {
+                A.end_state[0] = d.bs;
+                A.end_state[1] = d.pos;
+            }
         }
     }
 }
 
 }  // namespace
 
-// the batch decoders: K2s (slots of at most 4 KiB: a token-walk kernel and a move kernel), K2r
-// (lane per stream, slots < 64 KiB) or K2t (token-parallel wave per stream, longer slots), each
-// handing the streams it does not finish to the exact decoder; 's', 'r', 't' / 'w' force one
-// (tests, A/B; K2w is reached only this way)
-static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 's', 'r', 't', 'w'
+// the batch decoders: K2r (lane per stream, slots < 64 KiB) or K2t (token-parallel wave per stream,
+// longer slots), each handing the streams it does not finish to the exact decoder; 'r', 't' / 'w'
+// force one (tests, A/B; K2w is reached only this way)
+static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'r', 't', 'w'
 void select_decompress_variant(int v) { g_decompress_variant = v; }
 static int g_last_variant = 0;  // the first K2 kernel of the last batch decode ('e': exact alone)
 int last_decompress_variant() { return g_last_variant; }
 
-// [slow list: 2 * count + 32 words][K2w / K2t's deferred literals: 4 words + count * kDefSlots
-// records, or K2s's per-stream token bitmaps: count * kSmallRegion words (one or the other)]
+// [slow list: 2 * count + 32 words][K2w / K2t's deferred literals: 4 words + count * kDefSlots records]
 uint64_t decompress_workspace_words(uint64_t count) {
-    const uint64_t defer = 4 + count * (uint64_t)kDefSlots * (sizeof(DeferLit) / 4);
-    const uint64_t small = count * (uint64_t)kSmallRegion;
-    return 2 * count + 32 + (defer > small ? defer : small);
+    return 2 * count + 32 + 4 + count * (uint64_t)kDefSlots * (sizeof(DeferLit) / 4);
 }
 
 namespace {
@@ -312,24 +325,15 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     if (g_decompress_variant < 0) {
         const char *v = knob_str("EZ_K2");
         g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w'
-                               : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : (v && strcmp(v, "small") == 0 ? 's' : 0)));
+                               : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : 0));
     }
     const uint64_t exact_grid = a.count < 4096 ? a.count : 4096;
     // Slots under 64 KiB go to K2r's lane per stream; longer ones (C2, C4, the sweep's long streams) to
     // K2t (1 GiB batches, K2 ms, K2r / K2t: 8 KiB 1.89 / 4.99, 16 KiB 1.96 / 4.89, 32 KiB 3.50 / 5.06,
     // 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5) - / 7.0, 1 MiB (K2w 29.7) - / 14.4;
-    // C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms).  K2s (slots <= 4 KiB) is reached only when
-    // forced: at C1 it measured 1.15 ms against K2r's 0.46.
+    // C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms).
     const int v = a.force ? a.force : (g_decompress_variant != 0 ? g_decompress_variant : (a.max_out >= long_slot ? 't' : 'r'));
     g_last_variant = v;
-    if (v == 's') {
-        // K2s: the token walk writes each stream's bitmap of token starts (or hands it over), the move
-        // kernel decodes the streams the walk took
-        e = launch_decompress_small(a, a.slow + 2 * a.count + 32, st);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)exact_grid), dim3(64), 0, st, a);
-        return hipGetLastError();
-    }
     if (v == 't') {
         // K2t: token-parallel, a wave per stream; its hand-overs go to the exact decoder, the long
         // literals it defers are moved last (the exact decoder writes the same bytes for a stream it takes)

@@ -134,11 +134,9 @@ __device__ __forceinline__ int32_t run_step_of(int32_t per) { return per * (16 /
 
 // the advance of a rare form at input position p (h: its 16 bytes, the same on every lane):
 // the full parse; 2^30 (past any stream) when the stream goes to the exact decoder
-__device__ __attribute__((noinline)) int32_t rare_adv(const uint8_t *h, int32_t p, int32_t nb, int32_t lim32, int64_t limit, uint32_t *brk) {
+__device__ __attribute__((noinline)) int32_t rare_adv(const uint8_t *h, int32_t p, int32_t nb, int32_t lim32, int64_t limit) {
     K2Tok t;
     const int rr = k2_scan(lds16<0>(h), p, nb, lim32, limit, t);
-    // a Break meta (0x80, MetaBreak | MetaLen0): counted for the callers that must see it (Reader handles)
-    if (brk && rr == kParseSkip && h[0] == 0x80 && h[1] == (kMetaBreak | kMetaLen0) && threadIdx.x == 0) atomicAdd(brk, 1u);
     return __builtin_amdgcn_readfirstlane(rr == kParseHandOver ? (1 << 30) : t.adv);
 }
 
@@ -155,6 +153,15 @@ __device__ __attribute__((noinline)) int32_t rare_adv(const uint8_t *h, int32_t 
 #else
 #define HANDOVER(code) return false
 #endif
+
+// a hand-over because the output needs more than the slot: marked for a caller that sizes the slot
+// itself (a Reader handle's whole-stream decode retries with a larger one, and the exact decoder does
+// not re-decode the stream just to find the slot too small)
+#define HANDOVER_ROOM(code)                                   \
+    do {                                                      \
+        if (A.end_state && lane == 0) A.end_state[0] = -2;    \
+        HANDOVER(code);                                       \
+    } while (0)
 
 // stream s by the whole wave; false = hand it over to the exact decoder
 template <int32_t R>
@@ -254,7 +261,7 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
             }
             int32_t x = __builtin_amdgcn_readfirstlane((int32_t)ex[e]);
             if (x == e) {  // a rare form: the full parse (2^30: hand over)
-                x = e + __builtin_amdgcn_readfirstlane(rare_adv(inb + e, base + e, nb, lim32, limit, A.breaks));
+                x = e + __builtin_amdgcn_readfirstlane(rare_adv(inb + e, base + e, nb, lim32, limit));
                 if (lane == 0) ex[e] = (uint16_t)(x < 0xffff ? x : 0xffff);
             }
             e = x;
@@ -358,7 +365,8 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
                 const int32_t L0 = __builtin_amdgcn_readlane(L, 0), D0 = __builtin_amdgcn_readlane((int)tk.D, 0);
                 const bool cp0 = __builtin_amdgcn_readlane((int)tk.cp, 0) != 0;
                 const int32_t src0 = __builtin_amdgcn_readlane(q + tk.j, 0);
-                if ((uint32_t)pos + (uint32_t)L0 > (uint32_t)cap || (cp0 && bsl < 30 && (uint32_t)D0 > (1u << bsl))) HANDOVER(6);
+                if ((uint32_t)pos + (uint32_t)L0 > (uint32_t)cap) HANDOVER_ROOM(6);
+                if (cp0 && bsl < 30 && (uint32_t)D0 > (1u << bsl)) HANDOVER(6);
                 for (int32_t x = fl + 16 * lane; x < pos; x += 16 * kWave) {  // everything before it to HBM
                     const V16 v = rld<R>(ring, x);
                     if (x + 16 <= pos) st16v(out + x, v);
@@ -429,7 +437,15 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
             const bool in = lane < nr && tok;
             const int32_t total = __builtin_amdgcn_readlane(incl, nr - 1);
             const int32_t dst = pos + incl - L;
-            if ((uint32_t)pos + (uint32_t)total > (uint32_t)cap) HANDOVER(7);
+            // a Break meta (0x80, MetaBreak | MetaLen0) of the round: its output position, for a Reader
+            // handle's Reads (which stop there with ErrBreak, reader.go:312-313)
+            if (A.breaks && __ballot(has && lane < nr && rr == kParseSkip && ((uint32_t)h.lo & 0xffffu) == (0x80u | ((kMetaBreak | kMetaLen0) << 8)))) {
+                if (has && lane < nr && rr == kParseSkip && ((uint32_t)h.lo & 0xffffu) == (0x80u | ((kMetaBreak | kMetaLen0) << 8))) {
+                    const uint64_t at = atomicAdd((unsigned long long *)A.breaks, 1ull);
+                    if (at < A.breaks_cap) A.breaks[1 + at] = (uint64_t)dst;
+                }
+            }
+            if ((uint32_t)pos + (uint32_t)total > (uint32_t)cap) HANDOVER_ROOM(7);
             if (__ballot(in && tk.cp && bsl < 30 && tk.D > (1u << bsl))) HANDOVER(8);
             // ---- literals: all at once (their bytes from the staged window, or HBM past it)
             const bool lit = in && !tk.cp;
@@ -571,6 +587,10 @@ __device__ bool tok_one(const DecompressArgs &A, const uint64_t s, uint8_t *smem
     if (lane == 0) {
         A.out_size[s] = (uint64_t)pos;
         if (A.status) A.status[s] = EZ_OK;
+        if (A.end_state) {  // (one MetaReset, before any output: r.pos is the output since the start)
+            A.end_state[0] = bsl < 0 ? 0 : (int64_t)1 << bsl;
+            A.end_state[1] = pos;
+        }
     }
     return true;
 }

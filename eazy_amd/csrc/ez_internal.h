@@ -111,7 +111,13 @@ struct DecompressArgs {
     uint64_t defer_cap;       // records reserved
     uint64_t max_out;         // batch: host hint, largest output slot (0 = unknown)
     const uint32_t *todo;     // batch: [0] = count, [1..] = the streams to decode (nullptr = all)
-    uint32_t *breaks;         // batch, optional: counts the Break metas the decoders skip (reader.go:306-307)
+    // one-stream batches (count == 1, a Reader handle's whole-stream decode), optional, K2t and the exact
+    // decoder: breaks[0] counts the Break metas the decoders skip (reader.go:306-307) and breaks[1 ..
+    // breaks_cap] get their output positions (unordered); end_state gets {len(r.block), r.pos} at the end
+    // of the stream (the Reader's state after the last token, for a Read-by-Read continuation)
+    uint64_t *breaks;
+    uint64_t breaks_cap;
+    int64_t *end_state;
     int force;                // batch: the first K2 kernel ('r', 't', ...; 0 = the automatic / selected one)
 };
 
@@ -153,12 +159,6 @@ hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t s);
 hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t s);  // K2w, long streams
 hipError_t launch_defer_copy(const DecompressArgs &a, hipStream_t s);       // K2w's deferred literals
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t s);   // K2t, token-parallel wave per stream
-// K2s: small streams (slots <= kSmallOut), a token-walk kernel (lane per stream) writing a bitmap of
-// token starts into bm (kSmallRegion words per stream), then a move kernel (16 lanes per stream)
-constexpr int32_t kSmallOut = 4096;                 // output slots K2s takes
-constexpr int32_t kSmallIn = 6144;                  // compressed streams K2s takes (>= ez_compress_bound(4096))
-constexpr uint32_t kSmallRegion = 1 + kSmallIn / 32;  // [token count | hand over][one bit per input byte]
-hipError_t launch_decompress_small(const DecompressArgs &a, uint32_t *bm, hipStream_t s);
 bool lds_exchange_in_lane_order();  // the LDS property K1s-T32 relies on (checked once)
 bool lds_mskor_in_lane_order();     // the LDS property k1_lean's one-atomic visit relies on (checked once)
 bool lds_mskor64_in_lane_order();   // the same on 12-bit fields of 64-bit words (k1_lean<12>)

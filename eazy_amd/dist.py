@@ -44,6 +44,17 @@ def from_env() -> Rank:
                 int(os.environ.get("LOCAL_RANK", "0")))
 
 
+def _collective(r: Rank) -> bool:
+    """Whether the exchanges go through torch.distributed: always with more than one rank,
+    and at world size 1 too once a process group exists (so a one-GPU run still drives the
+    RCCL all-gather and all-reduce it would use at N GPUs, instead of a local shortcut)."""
+    if r.world > 1:
+        return True
+    import torch.distributed as dist
+
+    return dist.is_available() and dist.is_initialized()
+
+
 def shard_range(count: int, r: Rank) -> tuple[int, int]:
     """Global stream range [first, last) of rank r: contiguous, whole streams,
     sizes differing by at most one stream (strong scaling over one batch)."""
@@ -59,7 +70,7 @@ def exchange_sizes(local_sizes, count: int, r: Rank):
     shard in stream order) -> the global size table (count,) on every rank."""
     import torch
 
-    if r.world == 1:
+    if not _collective(r):
         return local_sizes.clone()
     import torch.distributed as dist
 
@@ -103,7 +114,7 @@ def gather_payload(packed_local, offsets, count: int, r: Rank, out=None, root: i
             out = torch.empty(max(1, spans[-1][0] + spans[-1][1]), dtype=torch.uint8, device=packed_local.device)
         base, n = spans[root]
         out[base : base + n].copy_(packed_local[:n])
-    if r.world == 1:
+    if not _collective(r) or r.world == 1:
         return out
     import torch.distributed as dist
 
@@ -124,7 +135,7 @@ def gather_payload(packed_local, offsets, count: int, r: Rank, out=None, root: i
 
 def reduce_max(values, r: Rank, device=None) -> list[float]:
     """Element-wise max over ranks (timing: the job ends with its slowest rank)."""
-    if r.world == 1:
+    if not _collective(r):
         return [float(v) for v in values]
     import torch
     import torch.distributed as dist
@@ -136,7 +147,7 @@ def reduce_max(values, r: Rank, device=None) -> list[float]:
 
 def reduce_sum(values, r: Rank, device=None) -> list[int]:
     """Element-wise sum over ranks (bytes processed / produced by the job)."""
-    if r.world == 1:
+    if not _collective(r):
         return [int(v) for v in values]
     import torch
     import torch.distributed as dist
@@ -147,7 +158,7 @@ def reduce_sum(values, r: Rank, device=None) -> list[int]:
 
 
 def barrier(r: Rank):
-    if r.world > 1:
+    if _collective(r):
         import torch.distributed as dist
 
         dist.barrier()

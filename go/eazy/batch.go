@@ -14,13 +14,52 @@ import (
 	"unsafe"
 )
 
-// compressBatch: one stream per buffer (one Write each).
+// compressBatch: one stream per buffer (one Write each), through ez_compress_batch_multi: the
+// batch is split into contiguous whole-stream shards over every visible device (Devices, when set),
+// one host thread and HIP stream per device, and the packed result comes back in host memory.
 func compressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
-	streams := make([][][]byte, len(bufs))
-	for k, b := range bufs {
-		streams[k] = [][]byte{b}
+	sizePanic(block, htable) // Writer.init writer.go:161-169, as NewWriter would
+	count := len(bufs)
+	if count == 0 {
+		return nil, nil
 	}
-	return compressStreams(streams, block, htable)
+	inOff := make([]uint64, count+1)
+	capacity := uint64(16)
+	for k, b := range bufs {
+		inOff[k+1] = inOff[k] + uint64(len(b))
+		capacity += uint64(C.ez_compress_bound(C.size_t(len(b))))
+	}
+	host := make([]byte, 0, inOff[count]+1)
+	for _, b := range bufs {
+		host = append(host, b...)
+	}
+	host = append(host, 0) // (a valid pointer for an all-empty batch)
+	packed := make([]byte, capacity)
+	packedOff := make([]uint64, count+1)
+	status := make([]int32, count)
+	var devs *C.int
+	ndev := 0
+	if len(Devices) > 0 {
+		cd := make([]C.int, len(Devices))
+		for k, d := range Devices {
+			cd[k] = C.int(d)
+		}
+		devs, ndev = &cd[0], len(cd)
+	}
+	st := C.ez_compress_batch_multi(C.int64_t(block), C.int64_t(htable), 0, (*C.uint8_t)(unsafe.Pointer(&host[0])),
+		(*C.uint64_t)(unsafe.Pointer(&inOff[0])), C.uint64_t(count), devs, C.int(ndev), (*C.uint8_t)(unsafe.Pointer(&packed[0])),
+		C.uint64_t(capacity), (*C.uint64_t)(unsafe.Pointer(&packedOff[0])), (*C.int32_t)(unsafe.Pointer(&status[0])))
+	if st != C.EZ_OK {
+		return nil, toErr(st, 0)
+	}
+	res := make([][]byte, count)
+	for k := range bufs {
+		if status[k] != 0 {
+			return nil, errors.Join(ErrDevice, toErr(C.int(status[k]), 0))
+		}
+		res[k] = packed[packedOff[k]:packedOff[k+1]:packedOff[k+1]]
+	}
+	return res, nil
 }
 
 // compressStreams stages the streams into device memory, runs K1 (stream k =

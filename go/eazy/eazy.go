@@ -480,9 +480,13 @@ func (r *Reader) more() error { // reader.go:516-543
 	return err
 }
 
-// CompressBatch compresses independent streams on the GPU: the result for
+// Devices lists the GPUs CompressBatch splits its batches over (contiguous whole-stream shards,
+// one per entry; an entry may repeat); empty: every visible device.
+var Devices []int
+
+// CompressBatch compresses independent streams on the GPUs: the result for
 // bufs[k] equals NewWriter(&buf, block, htable).Write(bufs[k]) into a fresh
-// buffer.  Inputs travel over pinned host memory; see INTEGRATION.md.
+// buffer.  The batch is sharded over Devices (every GPU by default); see INTEGRATION.md.
 func CompressBatch(bufs [][]byte, block, htable int) ([][]byte, error) {
 	return compressBatch(bufs, block, htable) // batch.go
 }

@@ -43,17 +43,21 @@ func TestCopy(t *testing.T) { // eazy_test.go:106-183
 
 func TestCompressBatch(t *testing.T) {
 	bufs := [][]byte{[]byte("level=info path=/api/v1 level=info path=/api/v2"), {}, bytes.Repeat([]byte("ab"), 3000)}
-	got, err := CompressBatch(bufs, MiB, 1024)
-	if err != nil {
-		t.Fatal(err)
-	}
-	for k, p := range bufs {
-		var buf bytes.Buffer
-		NewWriter(&buf, MiB, 1024).Write(p)
-		if len(p) > 0 && !bytes.Equal(got[k], buf.Bytes()) {
-			t.Fatalf("stream %d differs", k)
+	for _, devs := range [][]int{nil, {0, 0}, {0, 0, 0}} { // every device; two and three shards on device 0
+		Devices = devs
+		got, err := CompressBatch(bufs, MiB, 1024)
+		if err != nil {
+			t.Fatal(err)
+		}
+		for k, p := range bufs {
+			var buf bytes.Buffer
+			NewWriter(&buf, MiB, 1024).Write(p)
+			if len(p) > 0 && !bytes.Equal(got[k], buf.Bytes()) {
+				t.Fatalf("devices %v: stream %d differs", devs, k)
+			}
 		}
 	}
+	Devices = nil
 }
 
 // The reference's error and panic values, text included (reader.go:57-76, 303, 319;

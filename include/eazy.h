@@ -205,6 +205,28 @@ int ez_pack_batch(const uint8_t *slots, const uint64_t *slot_off, const uint64_t
 size_t ez_decompress_workspace(uint64_t count);
 int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, void *workspace, void *hip_stream);
 
+/* ---- host-memory batches over several devices (SURVEY §8b device_or_all) ----
+ * Streams share no state (writer.go:40-45, reader.go:17-40), so a batch splits into contiguous
+ * whole-stream shards, balanced by bytes, one per entry of `devices` (ndev entries; NULL or 0 =
+ * every visible device; an entry may repeat: two shards on one device, each on its own HIP
+ * stream); each shard runs on its own host thread: upload, the batch kernels, download.  All
+ * pointers are HOST pointers; the calls return when the output is in host memory.
+ *
+ * Compress: stream s = in[in_off[s] .. in_off[s+1]) as one Write to a fresh NewWriter(block,
+ * htable); packed gets the streams' outputs back to back, packed_off[count+1] their offsets
+ * (a host exclusive scan of the shards' packed sizes), status[count] (may be NULL) EZ_* per
+ * stream.  packed_cap < packed_off[count] -> EZ_ENOSPC with packed_off filled, packed untouched
+ * (sum of ez_compress_bound(n) always suffices). */
+int ez_compress_batch_multi(int64_t block, int64_t htable, int flags, const uint8_t *in, const uint64_t *in_off, uint64_t count,
+                            const int *devices, int ndev, uint8_t *packed, uint64_t packed_cap, uint64_t *packed_off,
+                            int32_t *status);
+/* Decompress: stream s = in[in_off[s] .. in_off[s+1]) read to EOF as NewReaderBytes does (Break
+ * metas skipped) into out[out_off[s] .. out_off[s+1]); out_size[count] bytes produced,
+ * status[count] (may be NULL) EZ_OK or the first error, as ez_decompress_batch. */
+int ez_decompress_batch_multi(int64_t block_size_limit, const uint8_t *in, const uint64_t *in_off, uint64_t count,
+                              const int *devices, int ndev, uint8_t *out, const uint64_t *out_off, uint64_t *out_size,
+                              int32_t *status);
+
 /* Introspection (no reference counterpart): the K1 kernel a batch of `count`
  * fresh streams of <= max_len bytes would run on the current device, as a
  * character: 's' K1s (parse + token writer; fresh streams with 2n <= block and
@@ -221,15 +243,14 @@ int ez_compress_kernel(int64_t block, int64_t htable, uint64_t max_len, uint64_t
  * back to the automatic choice.  Not thread-safe against concurrent calls. */
 int ez_select_compress_kernel(int kind);
 /* Testing / A-B measurement: the first K2 kernel of later batch decodes with a
- * workspace ('s' a token-walk kernel then 16 lanes per stream with the whole output in LDS, for
- * slots of at most 4 KiB; 'r' lane-per-stream with an LDS ring of recent output, 't'
+ * workspace ('r' lane-per-stream with an LDS ring of recent output, 't'
  * token-parallel wave per stream, 'w' wave per stream with a scalar token walk; 0 = automatic:
- * 't' when a slot is 64 KiB or more, else 'r' ('s' only when forced); the largest
+ * 't' when a slot is 64 KiB or more, else 'r'; the largest
  * slot is max_len when the caller gives it, else measured on the device, which waits for the
  * stream).  Streams the chosen kernel cannot take go on to the exact decoder. */
 int ez_select_decompress_kernel(int kind);
-/* Introspection: the first K2 kernel the last ez_decompress_batch call of this process ran ('s',
- * 'r', 't', 'w'; 'e' the exact decoder alone; 0 none yet). */
+/* Introspection: the first K2 kernel the last ez_decompress_batch call of this process ran
+ * ('r', 't', 'w'; 'e' the exact decoder alone; 0 none yet). */
 int ez_decompress_kernel_last(void);
 
 #ifdef __cplusplus

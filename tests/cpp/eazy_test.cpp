@@ -451,6 +451,40 @@ struct Recorder : IoWriter {  // an io.Writer keeping every call's bytes
     }
 };
 
+// Batches over a device list (ez_compress_batch_multi / ez_decompress_batch_multi through the C++
+// mirror): two shards on the one card ({0, 0}), three, and every device, each equal to one
+// NewWriter(MiB, 1024).Write per stream, and the streams decode back.
+static void TestBatchMulti() {
+    std::vector<Bytes> streams;
+    for (int s = 0; s < 57; s++) {
+        Bytes p;
+        for (int k = 0; k < (s % 9 == 0 ? 0 : 200 + 131 * s); k++)
+            p.push_back((uint8_t)("level=warn ip=10.0.3.7 path=/api/v2/users "[(k * 5 + s) % 41] ^ (k % 61 == 0 ? s : 0)));
+        streams.push_back(p);
+    }
+    std::vector<Bytes> want;
+    for (auto &p : streams) {
+        Buffer buf;
+        auto w = NewWriter(&buf, MiB, 1024);
+        if (!p.empty()) write_ok(*w, p);
+        else {
+            auto [n, err] = w->Write(p.data(), 0);
+            CHECK(n == 0 && err == Err::OK);
+        }
+        want.push_back(buf.b);
+    }
+    for (const std::vector<int> &devs : {std::vector<int>{0, 0}, std::vector<int>{0, 0, 0}, std::vector<int>{}}) {
+        std::vector<std::vector<uint8_t>> got;
+        CHECK(CompressBatchMulti(streams, MiB, 1024, got, devs) == Err::OK);
+        CHECK(got == want);
+        std::vector<uint64_t> slots;
+        for (auto &p : streams) slots.push_back(p.size());
+        std::vector<std::pair<std::vector<uint8_t>, Err>> dec;
+        CHECK(DecompressBatchMulti(got, slots, dec, devs) == Err::OK);
+        for (size_t k = 0; k < streams.size(); k++) CHECK(dec[k].second == Err::OK && dec[k].first == streams[k]);
+    }
+}
+
 static void TestWriteBatch() {  // Writer::WriteBatch == Write on each in turn (same sink calls)
     Bytes data;
     std::vector<uint64_t> ends;
@@ -625,6 +659,7 @@ int main(int argc, char **argv) {
         run("TestBatchMatchesWriter", TestBatchMatchesWriter);
         run("TestWriteBatch", TestWriteBatch);
         run("TestHandleLeak", TestHandleLeak);
+        run("TestBatchMulti", TestBatchMulti);
     }
     std::printf("%d/%d passed\n", g_run - g_fail, g_run);
     return g_fail ? 1 : 0;

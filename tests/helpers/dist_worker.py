@@ -8,7 +8,10 @@ per-stream compressed sizes into global offsets and sends its packed bytes to
 rank 0.  argv: out_dir mode.  mode "cpu": the shard's bytes come from the C
 oracle (no GPU in the container; the exchange code is the product's).  mode
 "gpu": the shard is compressed and packed by the HIP kernels on cuda:0 (K1 +
-K3 through the C-ABI), then the exchange runs on host copies (gloo).  Rank 0
+K3 through the C-ABI), then the exchange runs on host copies (gloo).  mode
+"nccl": the "gpu" shard, with the exchange on device tensors over RCCL (the
+backend bench.py's N>1 path uses; launched at world size 1 on a one-GPU box, the
+all-gather, payload gather and all-reduces still run as collectives).  Rank 0
 writes the global sizes, offsets and packed bytes to out_dir."""
 
 import os
@@ -64,17 +67,31 @@ def shard_packed(host, offs, mode):
 def main():
     out_dir, mode = sys.argv[1], sys.argv[2]
     R = ezd.from_env()
-    dist.init_process_group("gloo")
+    dev = None
+    if mode == "nccl":
+        torch.cuda.set_device(R.local)
+        dev = torch.device("cuda", R.local)
+        dist.init_process_group("nccl", device_id=dev)
+        assert dist.get_backend() == "nccl" and ezd._collective(R)
+    else:
+        dist.init_process_group("gloo")
     host, offs = global_batch()
     first, last = ezd.shard_range(COUNT, R)
-    packed, sizes = shard_packed(host, offs[first : last + 1], mode)
+    packed, sizes = shard_packed(host, offs[first : last + 1], "cpu" if mode == "cpu" else "gpu")
+    if dev is not None:
+        packed, sizes = packed.to(dev), sizes.to(dev)
     gsz = ezd.exchange_sizes(sizes, COUNT, R)
     goff = ezd.global_offsets(gsz)
     # this rank's shard lands at the global offset of its first stream
     assert int(goff[last]) - int(goff[first]) == int(sizes.sum())
     out = ezd.gather_payload(packed, goff, COUNT, R)
-    total = ezd.reduce_sum([int(sizes.sum())], R)[0]
+    total = ezd.reduce_sum([int(sizes.sum())], R, device=dev)[0]
     assert total == int(goff[-1])
+    slowest = ezd.reduce_max([1.0 + R.rank], R, device=dev)[0]
+    assert slowest == float(R.world)
+    ezd.barrier(R)
+    if dev is not None:
+        gsz, goff, out = gsz.cpu(), goff.cpu(), out.cpu() if out is not None else None
     if R.is_root:
         np.save(os.path.join(out_dir, "sizes.npy"), gsz.numpy())
         np.save(os.path.join(out_dir, "offsets.npy"), goff.numpy())

@@ -46,6 +46,12 @@ def test_no_cpu_fallback():
     lib = ez._lib()
     assert lib.ez_compress_batch(1 << 20, 1024, 0, None, None) == ez.EDEVICE
     assert lib.ez_decompress_batch(0, None, None, None) == ez.EDEVICE
+    import numpy as np
+
+    with pytest.raises(ez.DeviceError):
+        ez.compress_batch_multi(b"abcdefgh" * 8, np.array([0, 64]), devices=[0, 0])
+    with pytest.raises(ez.DeviceError):
+        ez.decompress_batch_multi(b"\x80\x10\x14\x01a", np.array([0, 5]), np.array([0, 16]))
 
 
 def test_writer_size_panics():

@@ -73,4 +73,4 @@ def test_cpp_dump_matches_python_dumper(tmp_path):
 @pytest.mark.gpu
 def test_cpp_full(cuda):
     out = _run()
-    assert "FAIL" not in out and "24/24 passed" in out
+    assert "FAIL" not in out and "25/25 passed" in out

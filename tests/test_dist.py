@@ -45,12 +45,12 @@ def test_global_logs_rank_independent():
     assert np.array_equal(whole[: 16 * 64], synth.logs(5, 16 * 64))
 
 
-def _run(tmp_path, mode):
+def _run(tmp_path, mode, nproc=2):
     sys.path.insert(0, os.path.join(HERE, "helpers"))
     import dist_worker as dw
 
     env = dict(os.environ, OMP_NUM_THREADS="1")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()),
            os.path.join(HERE, "helpers", "dist_worker.py"), str(tmp_path), mode]
     p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
@@ -121,3 +121,23 @@ def test_bench_rejects_world_mismatch():
 @pytest.mark.gpu
 def test_two_rank_exchange_gpu_kernels(tmp_path, cuda):
     _run(tmp_path, "gpu")
+
+
+@pytest.mark.gpu
+def test_rccl_exchange_world1(tmp_path, cuda):
+    """The RCCL binding on hardware, every round: one rank on the box's GPU with the nccl
+    backend (RCCL), the device bound before the process group starts, the shard compressed by
+    the HIP kernels, and the size all-gather (all_gather_into_tensor), payload gather and
+    all-reduces run as RCCL collectives (no world-1 shortcut once a group exists); the global
+    offsets and packed bytes must equal the oracle's packing of the whole batch."""
+    _run(tmp_path, "nccl", nproc=1)
+
+
+def test_collectives_without_group_shortcut():
+    """Without a process group a world-1 run needs no collective; with one it takes them."""
+    import torch
+
+    r = ezd.Rank(0, 1, 0)
+    assert not ezd._collective(r)
+    t = torch.arange(5, dtype=torch.int64)
+    assert ezd.exchange_sizes(t, 5, r).tolist() == t.tolist()

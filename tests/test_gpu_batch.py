@@ -43,7 +43,7 @@ def _run(cuda, bufs, block=MiB, htable=1024, magic=True):
     out2, sizes2, status2 = ez.decompress_batch(packed, poff, off, exact_only=True)
     mx = int(lens.max()) if len(lens) else 0
     others = [ez.decompress_batch(packed, poff, off, max_len=mx)]
-    for kind in ("s", "r", "w", "t"):
+    for kind in ("r", "w", "t"):
         ez.select_decompress_kernel(kind)
         try:
             others.append(ez.decompress_batch(packed, poff, off, max_len=mx))
@@ -376,3 +376,47 @@ def test_k1x_rounds(cuda, k1_kind):
     small = [_planted(rng, 80000, e, 4096, zeros=True) for e in (3, 12, 40)]
     for block, htable in ((4096, 16), (4096, 4096), (1024, 256)):
         _check(cuda, small, block, htable)
+
+
+def test_multi_device_batches_equal_one_device(cuda):
+    """ez_compress_batch_multi / ez_decompress_batch_multi (host memory, contiguous whole-stream
+    shards balanced by bytes, one host thread and HIP stream per device-list entry): the device
+    list [0, 0] (two shards on the one card), [0, 0, 0] and [0] give the single-device batch's
+    packing byte for byte (= the oracle's streams back to back) and the inputs back; ragged
+    lengths with empty streams, and fewer streams than shards (an empty shard)."""
+    import torch
+
+    import eazy_amd as ez
+    import oracle as orc
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(41)
+    lens = rng.integers(0, 9000, 301)
+    lens[::17] = 0
+    offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    host = synth.logs(43, int(offs[-1]))
+    want = [orc.compress(MiB, 1024, [host[offs[s] : offs[s + 1]].tobytes()]) for s in range(len(lens))]
+    want_packed = b"".join(want)
+    want_off = np.concatenate([[0], np.cumsum([len(w) for w in want])]).astype(np.int64)
+    # the single-device batch (device pointers, K1 + K3)
+    cb = ez.compress_batch(torch.from_numpy(host).to(cuda), torch.from_numpy(offs).to(cuda), MiB, 1024)
+    packed1, poff1 = ez.pack(cb)
+    torch.cuda.synchronize()
+    assert packed1[: int(poff1[-1])].cpu().numpy().tobytes() == want_packed
+    for devs in ([0], [0, 0], [0, 0, 0], None):
+        packed, poff, status = ez.compress_batch_multi(host, offs, MiB, 1024, devices=devs)
+        assert (status == 0).all() and poff.tolist() == want_off.tolist(), devs
+        assert packed.tobytes() == want_packed, devs
+        out_off = offs + 0
+        out, sizes, st = ez.decompress_batch_multi(packed, poff, out_off, devices=devs)
+        assert (st == 0).all() and sizes.tolist() == lens.tolist(), devs
+        assert out.tobytes() == host.tobytes(), devs
+    # fewer streams than shards
+    packed, poff, status = ez.compress_batch_multi(host[: offs[2]], offs[:3], MiB, 1024, devices=[0, 0, 0, 0])
+    assert packed.tobytes() == b"".join(want[:2]) and (status == 0).all()
+    # a slot one byte short: the stream's status is the decoder's, the others decode
+    out_off = offs.copy()
+    out_off[2:] -= 1
+    if lens[1] > 0:
+        out, sizes, st = ez.decompress_batch_multi(packed, poff, out_off[:3], devices=[0, 0])
+        assert st[0] == 0 and st[1] != 0

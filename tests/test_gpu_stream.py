@@ -122,7 +122,7 @@ def test_batch_decoder_errors_match_oracle(cuda):
     # the ring decoder with a small-slot hint on the same corpus
     cap = 8192
     ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-    for kind in ("s", "r", "w", "t"):
+    for kind in ("r", "w", "t"):
         ez.select_decompress_kernel(kind)
         try:
             out, sizes, status = ez.decompress_batch(comp, coff, ooff, max_len=cap)
@@ -171,7 +171,7 @@ def test_batch_decoders_on_damaged_streams(cuda):
     coff = torch.from_numpy(offs).to(cuda)
     for cap in (4096, 8192):
         ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-        for kind, kw in (("", {"max_len": cap}), ("s", {"max_len": cap}), ("r", {"max_len": cap}), ("w", {"max_len": cap}), ("t", {"max_len": cap}), ("", {}),
+        for kind, kw in (("", {"max_len": cap}), ("r", {"max_len": cap}), ("w", {"max_len": cap}), ("t", {"max_len": cap}), ("", {}),
                          ("", {"exact_only": True})):
             ez.select_decompress_kernel(kind)
             try:
@@ -228,7 +228,7 @@ def test_batch_decoders_ring_edge_distances(cuda):
     coff = torch.from_numpy(offs).to(cuda)
     cap = 72 << 10
     ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
-    for kind in ("", "s", "w", "r", "t"):
+    for kind in ("", "w", "r", "t"):
         ez.select_decompress_kernel(kind)
         try:
             out, sizes, status = ez.decompress_batch(comp, coff, ooff, max_len=cap)
@@ -459,9 +459,9 @@ def test_handle_writes_k1l_and_general(cuda, block, ht):
     assert outs[1] == want, "general kernel"
 
 
-def test_k2s_checks_and_forms(cuda):
-    """K2s (the token walk + the 16-lane move kernel) on hand-built small streams: every check
-    the move kernel makes hands the stream to the exact decoder with the reference's result —
+def test_fast_decoders_checks_and_forms(cuda):
+    """The fast decoders (K2r, K2t, K2w) on hand-built small streams: every check they make
+    hands the stream to the exact decoder with the reference's result —
     slots one byte too small, BlockSizeLimit below a token's length, a copy farther than the
     window (MetaReset with a 32-byte block), a token before the window is set, a reset after
     output — and the long forms it parses itself (Len1/Len2 literals and copies, Off1/Off2/
@@ -502,7 +502,7 @@ def test_k2s_checks_and_forms(cuda):
     for cap, limit in ((4096, 0), (max(lens), 0), (max(lens) - 1, 0), (4096, 64), (4096, 250)):
         ooff = torch.arange(len(ins) + 1, dtype=torch.int64, device=cuda) * cap
         res = {}
-        for kind in ("s", ""):
+        for kind in ("r", "t", "w", ""):
             ez.select_decompress_kernel(kind)
             try:
                 res[kind] = ez.decompress_batch(comp, coff, ooff, block_size_limit=limit, max_len=cap)
@@ -517,16 +517,18 @@ def test_k2s_checks_and_forms(cuda):
                 n = int(sizes[s])
                 assert torch.equal(out[s * cap : s * cap + n], ex[0][s * cap : s * cap + n]), (kind, cap, limit, s)
         if limit == 0:
-            _cmp_oracle(ins, cap, res["s"][0].cpu().numpy(), res["s"][1].cpu().numpy(), res["s"][2].cpu().numpy())
+            for kind in ("r", "t"):
+                _cmp_oracle(ins, cap, res[kind][0].cpu().numpy(), res[kind][1].cpu().numpy(), res[kind][2].cpu().numpy())
 
 
 def test_reader_whole_decode_matches_read_by_read(cuda):
     """NewReaderBytes decodes the whole stream on its first Read (ez_reader_set_whole) and serves
     the Reads from it; with set_whole(0) (NewReader's mode) it decodes Read by Read.  Same bytes and the
     same error sequence for a multi-block stream (Reset metas at every 1 MiB block), a stream with a
-    version header, one with a Break meta in the middle (decode-ahead declines: ErrBreak at the same
-    Read), a truncated stream and one ending in an unsupported meta (both decline: the exact
-    decoder's error)."""
+    version header, streams with Break metas (in the middle, several back to back, at the very start and
+    at the end: the Reads stop at each with ErrBreak, from the decoders' recorded break positions), a
+    stream that expands more than 20x (the device slot grows past 8x the input), a truncated stream and
+    one ending in an unsupported meta (both decline: the exact decoder's error)."""
     import eazy_amd as ez
     import impls
     from eazy_amd import synth
@@ -535,20 +537,22 @@ def test_reader_whole_decode_matches_read_by_read(cuda):
     plain = synth.logs(91, 3 << 20).tobytes()
     chunks = [plain[k : k + 200_000] for k in range(0, len(plain), 200_000)]
 
-    def stream(brk=False, hdr=False):
+    def stream(brk=(), hdr=False, data=chunks):
         w = G.W(1 << 20, 1024)
         if hdr:
             w.append_magic = True
             assert w.write_header() == ez.OK
-        for k, c in enumerate(chunks):
-            assert w.write(c) == (len(c), ez.OK)
-            if brk and k == len(chunks) // 2:
+        for k, c in enumerate(data):
+            for _ in range(brk.count(k)):
                 assert w.write_break() == ez.OK
+            assert w.write(c) == (len(c), ez.OK)
+        for _ in range(brk.count(len(data))):
+            assert w.write_break() == ez.OK
         return w.sink
 
     def read_all(r, size):
         out, errs = bytearray(), []
-        for _ in range(4000):
+        for _ in range(100000):
             got, err = r.read(size)
             out += got
             errs.append(err)
@@ -557,24 +561,88 @@ def test_reader_whole_decode_matches_read_by_read(cuda):
         return bytes(out), errs
 
     clean = stream()
-    cases = {"clean": (clean, True), "header": (stream(hdr=True), True), "break": (stream(brk=True), False),
-             "truncated": (clean[: len(clean) - 7], False)}
-    cases["unsupported_meta"] = (clean + bytes([K.Meta, 0x40 | K.MetaLen0]), False)
-    for name, (comp, ahead) in cases.items():
-        for size in (4096, 1 << 20):
+    # 16 MiB of a short pattern with a few varied bytes: > 20x expansion
+    dense_parts = [(b"abcdefgh" * 65536)[: 1 << 19] + bytes([k]) * 64 for k in range(32)]
+    dense = stream(data=dense_parts)
+    assert len(b"".join(dense_parts)) > 20 * len(dense)
+    cases = {"clean": (clean, True, plain, 0), "header": (stream(hdr=True), True, plain, 0),
+             "break": (stream(brk=(len(chunks) // 2,)), True, plain, 1),
+             "breaks": (stream(brk=(0, 3, 3, 3, 7, len(chunks))), True, plain, 6),
+             "dense": (dense, True, b"".join(dense_parts), 0),
+             "truncated": (clean[: len(clean) - 7], False, None, 0)}
+    cases["unsupported_meta"] = (clean + bytes([K.Meta, 0x40 | K.MetaLen0]), False, None, 0)
+    for name, (comp, ahead, want_plain, nbrk) in cases.items():
+        for size in (4096, 200_000, 1 << 20):
             rb = G.Rb(comp)
             got, errs = read_all(rb, size)
-            assert rb.r.whole_decoded == ahead, name
+            assert rb.r.whole_decoded == ahead, (name, size)
             rx = G.Rb(comp)
             ez._lib().ez_reader_set_whole(rx.r._h, 0)  # the same handle decoding Read by Read
             want, werrs = read_all(rx, size)
             assert not rx.r.whole_decoded
             assert errs == werrs, (name, size, errs[-3:], werrs[-3:])
             assert got == want, (name, size)
-            if name in ("clean", "header", "break"):
-                assert got == plain and errs[-1] == ez.EOF, name
-            if name == "break":
-                assert errs.count(ez.EBREAK) == 1
+            if want_plain is not None:
+                assert got == want_plain and errs[-1] == ez.EOF, name
+            assert errs.count(ez.EBREAK) == nbrk, (name, size)
+
+
+def test_reader_whole_decode_then_more_input(cuda):
+    """A Reader set after NewReaderBytes (reader.go:27: a public field) supplies input after the
+    decoded stream: the handle goes on Read by Read from the Reader's state at the stream's end
+    (window size, position, the window's history), so copies in the new input that reach back into
+    the first part decode exactly as on a handle that decoded everything Read by Read."""
+    import eazy_amd as ez
+    import impls
+    from eazy_amd import synth
+
+    G = impls.Gpu()
+    plain = synth.logs(93, 1 << 20).tobytes()
+    w = G.W(1 << 16, 1024)
+    assert w.write(plain[: 600_000]) == (600_000, ez.OK)
+    first = bytes(w.sink)
+    assert w.write(plain[600_000:]) == (len(plain) - 600_000, ez.OK)
+    second = bytes(w.sink)[len(first) :]
+    results = []
+    for whole in (1, 0):
+        rb = G.Rb(first)
+        ez._lib().ez_reader_set_whole(rb.r._h, whole)
+        out, errs = bytearray(), []
+        for k in range(10000):
+            if k == 40:  # part-way through the first part: the rest comes from an io.Reader
+                rb.r.Reader = impls._Src(second, True)
+                rb.r.BufferSize = 64 << 10
+            got, err = rb.read(8192)
+            out += got
+            errs.append(err)
+            if err not in (ez.OK, ez.EBREAK):
+                break
+        results.append((bytes(out), errs, rb.r.whole_decoded))
+    (a, ea, _), (b, eb, _) = results
+    assert a == b == plain and ea == eb and ea[-1] == ez.EOF
+
+
+def test_reader_whole_decode_reset(cuda):
+    import eazy_amd as ez
+    import impls
+    from eazy_amd import synth
+
+    G = impls.Gpu()
+    plain = synth.logs(91, 3 << 20).tobytes()
+    w = G.W(1 << 20, 1024)
+    for k in range(0, len(plain), 200_000):
+        assert w.write(plain[k : k + 200_000])[1] == ez.OK
+    clean = w.sink
+
+    def read_all(r, size):
+        out = bytearray()
+        for _ in range(100000):
+            got, err = r.read(size)
+            out += got
+            if err not in (ez.OK, ez.EBREAK):
+                break
+        return bytes(out), err
+
     # ResetBytes starts a new whole decode; Reset(io.Reader) goes back to Read by Read
     rb = G.Rb(clean)
     assert rb.read(10)[0] == plain[:10] and rb.r.whole_decoded
