@@ -252,6 +252,9 @@ struct ez_writer {
     int append_magic = 1;
     int ver = 0;
     bool pristine = true;  // isreset(): nothing emitted since the last reset
+    // the device's ring and table may hold a Write that failed and was not reset (writer_zero itself
+    // failed): the next call resets them first, and fails until that works
+    bool tainted = false;
     int64_t pos = 0;       // w.pos
     int last_panic = EZ_PANIC_NONE;  // the reference panic behind the last EZ_EINVAL
     // dev: [input | in_off[2] out_off[2] out_size status write_idx[2] | write_end[k] | write_out[k] | output]
@@ -269,8 +272,12 @@ int writer_zero(ez_writer *w) {
     EZ_HIP(hipStreamSynchronize(w->stream));
     w->pos = 0;
     w->pristine = true;
+    w->tainted = false;
     return EZ_OK;
 }
+
+// a call that changes the device history starts from a clean one
+int writer_clean(ez_writer *w) { return w->tainted ? writer_zero(w) : EZ_OK; }
 
 int writer_alloc(ez_writer *w, int64_t bs, int64_t hs) {
     if (w->ring.ensure((size_t)bs)) return EZ_EDEVICE;
@@ -325,7 +332,7 @@ extern "C" int ez_writer_set_version(ez_writer *w, int ver) {
     return EZ_OK;
 }
 
-extern "C" int ez_writer_is_reset(const ez_writer *w) { return w->pristine ? 1 : 0; }
+extern "C" int ez_writer_is_reset(const ez_writer *w) { return w->pristine || w->tainted ? 1 : 0; }
 
 extern "C" int ez_writer_last_panic(const ez_writer *w) { return w->last_panic; }
 
@@ -405,6 +412,7 @@ int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t
         boff += b;
     }
     EZ_HIP(hipMemcpyAsync(D, H, o_meta + 6 * 8 * k, hipMemcpyHostToDevice, w->stream));
+    w->tainted = true;  // (cleared when the call completes, or by the reset of a failed one)
     hipError_t he = hipSuccess;
     for (size_t j = 0; j < k && he == hipSuccess; j++) {
         const uint64_t len = ends[j] - (j ? ends[j - 1] : 0);
@@ -438,6 +446,7 @@ int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t
     }
     w->pos += (int64_t)n;
     w->pristine = false;
+    w->tainted = false;
     return EZ_OK;
 }
 
@@ -452,6 +461,12 @@ int writer_run(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, u
     // checked before anything reaches the device: the kernel advances the handle's ring and table, so a
     // call that could not return its bytes must not run at all (a retry then sees the same history)
     if (cap < bound) return EZ_ENOSPC;
+    {
+        DeviceGuard g(w->device);
+        if (!g.ok) return EZ_EDEVICE;
+        const int z = writer_clean(w);
+        if (z) return z;
+    }
     if (k >= 1) {  // K1L on the handle's ring and table, when every Write qualifies
         const int e = writer_run_long(w, p, ends, k, out, cap, out_ends, bound);
         if (e >= 0) return e;
@@ -495,6 +510,7 @@ int writer_run(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, u
     }
     // from the launch on, the device history may already hold p: any failure restarts the stream
     // (as Go does after a failed sink write, writer.go:391-393), so later Writes stay exact
+    w->tainted = true;
     hipError_t he = ez::launch_compress(a, w->stream);
     // status, sizes and output back at once (the bound, not the exact size: small Writes)
     if (he == hipSuccess)
@@ -529,6 +545,7 @@ int writer_run(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t k, u
     }
     w->pos += (int64_t)n;
     w->pristine = false;
+    w->tainted = false;
     return EZ_OK;
 }
 
@@ -552,6 +569,12 @@ extern "C" int ez_writer_write_batch(ez_writer *w, const uint8_t *p, const uint6
 
 extern "C" int ez_writer_header(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n) {
     *out_n = 0;
+    if (w->tainted) {
+        DeviceGuard g(w->device);
+        if (!g.ok) return EZ_EDEVICE;
+        const int z = writer_clean(w);
+        if (z) return z;
+    }
     if (!w->pristine) return EZ_OK;
     uint8_t h[16];
     const size_t k = header_bytes(h, w->append_magic, w->ver, w->bs);
@@ -564,6 +587,12 @@ extern "C" int ez_writer_header(ez_writer *w, uint8_t *out, size_t cap, size_t *
 
 extern "C" int ez_writer_break(ez_writer *w, uint8_t *out, size_t cap, size_t *out_n) {
     *out_n = 0;
+    if (w->tainted) {
+        DeviceGuard g(w->device);
+        if (!g.ok) return EZ_EDEVICE;
+        const int z = writer_clean(w);
+        if (z) return z;
+    }
     uint8_t h[32];
     size_t k = 0;
     if (w->pristine) k = header_bytes(h, w->append_magic, w->ver, w->bs);
@@ -733,7 +762,8 @@ int reader_ahead(ez_reader *r, const uint8_t *b, size_t b_len) {
         a.block_size_limit = r->limit;
         a.slow = r->a_ws.as<uint32_t>();
         a.max_out = cap;
-        a.force = 't';  // one stream: the token-parallel wave
+        // one stream: K2j (chip-wide) for a long one, else the token-parallel wave
+        a.force = b_len >= ((size_t)16 << 10) ? 'j' : 't';
         if (ez::launch_decompress(a, r->stream) != hipSuccess) return 0;
         if (hipMemcpyAsync(m, r->a_meta.p, sizeof m, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
         if (hipMemcpyAsync(&nbrk, r->a_brk.p, 8, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
@@ -1011,7 +1041,7 @@ extern "C" int ez_select_compress_kernel(int kind) {
 }
 
 extern "C" int ez_select_decompress_kernel(int kind) {
-    if (kind != 0 && kind != 'r' && kind != 'w' && kind != 't') return EZ_EINVAL;
+    if (kind != 0 && kind != 'r' && kind != 'w' && kind != 't' && kind != 'j') return EZ_EINVAL;
     ez::select_decompress_variant(kind);
     return EZ_OK;
 }

@@ -332,8 +332,16 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     // K2t (1 GiB batches, K2 ms, K2r / K2t: 8 KiB 1.89 / 4.99, 16 KiB 1.96 / 4.89, 32 KiB 3.50 / 5.06,
     // 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5) - / 7.0, 1 MiB (K2w 29.7) - / 14.4;
     // C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms).
-    const int v = a.force ? a.force : (g_decompress_variant != 0 ? g_decompress_variant : (a.max_out >= long_slot ? 't' : 'r'));
+    int v = a.force ? a.force : (g_decompress_variant != 0 ? g_decompress_variant : (a.max_out >= long_slot ? 't' : 'r'));
+    if (v == 'j' && !jump_applies(a)) v = 't';
     g_last_variant = v;
+    if (v == 'j') {
+        // K2j: few long streams with the whole chip; its hand-overs go to the exact decoder
+        e = launch_decompress_jump(a, st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)exact_grid), dim3(64), 0, st, a);
+        return hipGetLastError();
+    }
     if (v == 't') {
         // K2t: token-parallel, a wave per stream; its hand-overs go to the exact decoder, the long
         // literals it defers are moved last (the exact decoder writes the same bytes for a stream it takes)

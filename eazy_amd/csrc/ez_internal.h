@@ -158,6 +158,10 @@ int last_decompress_variant();  // the first K2 kernel of the last batch decode
 hipError_t launch_decompress_ring(const DecompressArgs &a, hipStream_t s);
 hipError_t launch_decompress_wave(const DecompressArgs &a, hipStream_t s);  // K2w, long streams
 hipError_t launch_defer_copy(const DecompressArgs &a, hipStream_t s);       // K2w's deferred literals
+// K2j (ez_decompress_jump.hip): batches of at most 1,024 streams, chip-wide token starts, token
+// records and pointer jumping over the copied bytes; streams it cannot take go to slow
+bool jump_applies(const DecompressArgs &a);
+hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t s);
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t s);   // K2t, token-parallel wave per stream
 bool lds_exchange_in_lane_order();  // the LDS property K1s-T32 relies on (checked once)
 bool lds_mskor_in_lane_order();     // the LDS property k1_lean's one-atomic visit relies on (checked once)

@@ -43,7 +43,7 @@ def _run(cuda, bufs, block=MiB, htable=1024, magic=True):
     out2, sizes2, status2 = ez.decompress_batch(packed, poff, off, exact_only=True)
     mx = int(lens.max()) if len(lens) else 0
     others = [ez.decompress_batch(packed, poff, off, max_len=mx)]
-    for kind in ("r", "w", "t"):
+    for kind in ("r", "w", "t", "j"):
         ez.select_decompress_kernel(kind)
         try:
             others.append(ez.decompress_batch(packed, poff, off, max_len=mx))

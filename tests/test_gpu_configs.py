@@ -197,7 +197,7 @@ def test_k2w_literal_longer_than_the_hint(cuda):
     comp = torch.from_numpy(np.frombuffer(b"".join(want) + bytes(64), np.uint8).copy()).to(dev)
     coff = torch.tensor([0, len(want[0]), len(want[0]) + len(want[1])], dtype=torch.int64, device=dev)
     ooff = torch.tensor([0, len(bufs[0]), len(bufs[0]) + len(bufs[1])], dtype=torch.int64, device=dev)
-    for kind in ("w", "t"):
+    for kind in ("w", "t", "j"):
         ez.select_decompress_kernel(kind)
         try:
             out, sz, st = ez.decompress_batch(comp, coff, ooff, max_len=64 << 10)
@@ -344,7 +344,7 @@ def test_k2t_copy_chains_within_rounds(cuda):
     d_coff, d_offs = torch.from_numpy(coff).to(cuda), torch.from_numpy(offs).to(cuda)
     _, sz0, st0 = ez.decompress_batch(comp, d_coff, d_offs, exact_only=True)
     assert st0.abs().sum().item() == 0
-    for kind in ("t", "w", "r", ""):
+    for kind in ("t", "w", "r", "j", ""):
         ez.select_decompress_kernel(kind)
         try:
             out, sz, st = ez.decompress_batch(comp, d_coff, d_offs, max_len=max(lens))
@@ -389,7 +389,7 @@ def test_k2t_deferred_literal_neighbours(cuda):
         offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
         comp = torch.from_numpy(np.frombuffer(b"".join(want) + bytes(64), np.uint8).copy()).to(cuda)
         d_coff, d_offs = torch.from_numpy(coff).to(cuda), torch.from_numpy(offs).to(cuda)
-        for kind in ("t", "w", ""):
+        for kind in ("t", "w", "j", ""):
             ez.select_decompress_kernel(kind)
             try:
                 out, sz, st = ez.decompress_batch(comp, d_coff, d_offs)
@@ -431,3 +431,64 @@ def test_decoder_routing_without_hint(cuda):
             got = out[: int(offs[-1])].cpu().numpy().tobytes()
             for s, b in enumerate(bufs):
                 assert got[offs[s] : offs[s + 1]] == b, f"{kind}: stream {s} differs"
+
+
+@pytest.mark.gpu
+def test_k2j_chip_wide_decode(cuda):
+    """K2j (token starts from speculative 2 KiB chunks, token records, pointer jumping over the
+    copied bytes) on the shapes its steps must get right, each stream against the oracle (bytes,
+    sizes, statuses): copy-of-copy chains across a whole long stream (log templates: every event's
+    copy reads the previous event's), runs with distance < 16, OffLong-0 zero regions, copies
+    reaching before the stream start, long literals (an entry that skips chunks), padding and
+    Break metas between tokens, a stream ending in the middle of a token, a MetaReset after
+    output (declines: the exact decoder's error), a slot one byte short, an empty stream; in one
+    batch and one stream per batch."""
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    rng = np.random.default_rng(123)
+    hdr = b"\x80\x02eazy\x80\x10\x14"
+    logs = synth.logs(127, 3 << 20).tobytes()
+    f = rng.standard_normal(300000).astype(np.float32).tobytes()
+    zero = bytearray(400000)
+    for q in range(0, len(zero), 37):
+        zero[q] = q & 0xFF
+    ins = [orc.compress(MiB, 1024, [logs]),                                   # 3 MiB of logs: deep chains
+           orc.compress(MiB, 1024, [_chain_stream(rng, 500000)]),             # runs, overlapping copies
+           orc.compress(MiB, 1024, [f]),                                      # one 1.2 MB literal
+           orc.compress(MiB, 1024, [bytes(zero)]),                            # zero runs and patterns
+           orc.compress(MiB, 1024, [logs[:70000], f[:5000], logs[70000:90000]]),  # multi-Write
+           hdr + b"\x87\xff\x00" + b"\x03abc" + b"\x8a\xff\x05",          # a zero region, a run
+           hdr + b"\x03abc" + b"\x86\x04" + b"\x02xy" + b"\x88\x40",        # copies from before the start
+           orc.compress(MiB, 1024, [logs[:9000]]) + b"\x00" * 40 + b"\x80\x1f" + b"\x80\x1f" + b"\x05hello",
+           orc.compress(MiB, 1024, [logs[:50000]])[:-3],                      # ends inside a token
+           orc.compress(MiB, 1024, [logs[:3000]]) + b"\x80\x10\x14\x02ab",   # MetaReset after output
+           b""]
+    lens = [len(orc.decompress(x, cap=8 << 20)[0]) for x in ins]
+    for cap_delta in (0, -1):
+        caps = [n + 64 for n in lens]
+        caps[0] = lens[0] + cap_delta  # (a slot one byte short: the exact decoder's ENOSPC)
+        for batch in ([list(range(len(ins)))] + [[k] for k in range(len(ins))] if cap_delta == 0 else [list(range(len(ins)))]):
+            sub = [ins[k] for k in batch]
+            scap = [caps[k] for k in batch]
+            coff = np.concatenate([[0], np.cumsum([len(x) for x in sub])]).astype(np.int64)
+            ooff = np.concatenate([[0], np.cumsum(scap)]).astype(np.int64)
+            comp = torch.from_numpy(np.frombuffer(b"".join(sub) + bytes(64), np.uint8).copy()).to(cuda)
+            d_coff, d_ooff = torch.from_numpy(coff).to(cuda), torch.from_numpy(ooff).to(cuda)
+            ez.select_decompress_kernel("j")
+            try:
+                out, sz, st = ez.decompress_batch(comp, d_coff, d_ooff, max_len=max(scap))
+                torch.cuda.synchronize()
+                assert ez.decompress_kernel_last() == "j"
+            finally:
+                ez.select_decompress_kernel("")
+            ex = ez.decompress_batch(comp, d_coff, d_ooff, exact_only=True)
+            torch.cuda.synchronize()
+            assert torch.equal(st, ex[2]) and torch.equal(sz, ex[1]), (batch, st.tolist(), ex[2].tolist())
+            o = out.cpu().numpy()
+            for i, k in enumerate(batch):
+                want, err, _ = orc.decompress(ins[k], cap=scap[i])
+                n = int(sz[i])
+                assert o[ooff[i] : ooff[i] + n].tobytes() == want[:n], (k, n)

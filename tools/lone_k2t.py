@@ -1,7 +1,7 @@
 """Decode time of ONE long log stream on the batch path (count = 1, the Reader handle's
-decode-ahead shape): K2t forced, CUDA-event timing over a few launches.  With EZ_LIB pointing at
+decode-ahead shape): K2t forced (or K2j with --kind j), CUDA-event timing over a few launches.  With EZ_LIB pointing at
 an experiment build (make -C eazy_amd exp X=<bits>) the EZ_EXP phase skips of K2t give the
-phase split (wrong bytes, timing only).  Usage: python tools/lone_k2t.py [MiB] [--check]"""
+phase split (wrong bytes, timing only).  Usage: python tools/lone_k2t.py [MiB] [--check] [--kind t|j]"""
 
 import os
 import sys
@@ -26,7 +26,8 @@ def main():
     coff = torch.tensor([0, len(comp)], dtype=torch.int64, device=dev)
     cap = 8 * len(comp) + 4096
     ooff = torch.tensor([0, cap], dtype=torch.int64, device=dev)
-    ez.select_decompress_kernel("t")
+    kind = sys.argv[sys.argv.index("--kind") + 1] if "--kind" in sys.argv else "t"
+    ez.select_decompress_kernel(kind)
     out, sizes, status = ez.decompress_batch(c, coff, ooff)
     torch.cuda.synchronize()
     if "--check" in sys.argv:
@@ -41,7 +42,7 @@ def main():
         torch.cuda.synchronize()
         ts.append(e0.elapsed_time(e1))
     ms = min(ts)
-    print(f"lib={os.path.basename(ez.LIB_PATH)} {mib} MiB stream ({len(comp)} B compressed): {ms:.2f} ms, "
+    print(f"lib={os.path.basename(ez.LIB_PATH)} K2{ez.decompress_kernel_last()} {mib} MiB stream ({len(comp)} B compressed): {ms:.2f} ms, "
           f"{len(plain) / ms / 1e3 / 1.048576:.1f} MiB/s, status {int(status[0])}")
 
 
