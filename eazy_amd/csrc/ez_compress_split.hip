@@ -837,6 +837,7 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
     int err = 0;
     bool live = false, pending = false;
     uint64_t *rec = recs;
+    V16 z0{0, 0}, z1{0, 0}, z2{0, 0};
     typename std::conditional<LW, WinLds<W40 ? 64 : 80>, WinRoll>::type wr;
     if constexpr (LW) wr.wl = wl;
     // iterations left to the wave (SALU): every stream opened adds its parse's bound, so a correct
@@ -879,6 +880,15 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
         i = done = nrec = 0;
         rec = recs + (pending ? s : 0) * rcap;
         wr.init(p, n, lj, live);
+        // the bytes around stream position 0, the candidate of every zero table entry:
+        // judged without a load (a load for every lane measured 2.35 against 2.00 ms at C1: the
+        // vector-memory path is the parse's busiest)
+        z0 = z1 = z2 = V16{0, 0};
+        if (live) {
+            if constexpr (W40) bytes48(L, p, 0, z0, z1, z2);
+            else bytes32(L, p, 0, z0, z1);
+            z0.lo = 0;
+        }
     };
     open();
     budget += (int64_t)(4 * A.max_len + 64) * S;
@@ -903,11 +913,15 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
             if (PERSIST && __ballot(pending) != 0) continue;
             break;
         }
-        if (--budget < 0) {
+        if (budget < 0) {
             if (live) err = EZ_ESTUCK;
             live = false;
             continue;
         }
+        // the parse, until one of the groups' streams ends (the bookkeeping above stays out of it)
+        const uint64_t lm = __ballot(live);
+        do {
+        budget--;
         if constexpr (W40) wr.bytes48(i, g, lj, w0, w1, w2);
         else wr.bytes(i, g, lj, w0, w1);
         const int32_t nvalid = n - 3 - i < G ? n - 3 - i : G;
@@ -927,14 +941,14 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
             const int32_t d = PredZ<G - 1>::get(valid ? h + 1 : 0u, 0);
             cand = valid ? (d ? x - d : tv) : 0;
         }
-        // the candidate's bytes, every lane (a zero table entry is stream position 0, SURVEY A.2:
-        // its bytes load like any other; the 64 bytes before a stream are readable)
-        V16 c0, c1, c2{0, 0};
-        if constexpr (W40) bytes48(L, p, cand, c0, c1, c2);
-        else if (kFwdCap == 20) bytes28(L, p, cand, c0, c1);
-        else bytes32(L, p, cand, c0, c1);
-        // bytes before the stream start are the fresh ring's zeros (rare: a branch)
-        if (__builtin_expect(cand < 8, 0)) c0.lo = cand == 0 ? 0ull : c0.lo & (~0ull << (8 * (8 - cand)));
+        V16 c0 = z0, c1 = z1, c2 = z2;
+        if (cand != 0) {
+            if constexpr (W40) bytes48(L, p, cand, c0, c1, c2);
+            else if (kFwdCap == 20) bytes28(L, p, cand, c0, c1);
+            else bytes32(L, p, cand, c0, c1);
+            // bytes before the stream start are the fresh ring's zeros (rare: a branch)
+            if (__builtin_expect(cand < 8, 0)) c0.lo &= ~0ull << (8 * (8 - cand));
+        }
         if (prio & 1) __builtin_amdgcn_s_setprio(0);
 
         // ---- capped judgement, writer.go:219-301 (window) and :441-463 (writeRunlen)
@@ -976,12 +990,14 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
         const uint32_t am = (uint32_t)(am64 >> (G * g)) & 0xffffu;
         const int a = am ? __builtin_ctz(am) : -1;
         const bool act = live && a >= 0;
-        // the group's next position (and whether the acceptor needs an exact extension)
-        const int32_t pack = nx | (ext << 28);
+        // the group's next position, whether the acceptor needs an exact extension, and whether it
+        // makes the i+1 insert (a window match, writer.go:315-318)
+        const bool ins1 = !rl && !zr && x + 1 + 4 <= n;
+        const int32_t pack = nx | (ext << 28) | ((int32_t)ins1 << 30);
         // (one ds_bpermute from each group's first acceptor: fewer VALU than four v_readlane + selects)
         const int32_t sel = __builtin_amdgcn_ds_bpermute(4 * (G * g + (a < 0 ? 0 : a)), pack);
         int32_t nxt = sel & 0x0fffffff;
-        if (__ballot(act && (sel >> 28) != 0) != 0) {
+        if (__ballot(act && ((sel >> 28) & 3) != 0) != 0) {
             // rare: a saturated count; exact lengths by the whole group (as k1_parse)
             // the acceptor's candidate, capped backward count (<= 8) and branch
             const int32_t info = cand | (((zr ? cand : x) - lit) << 16) | ((int32_t)rl << 29) | ((int32_t)zr << 30);
@@ -1007,16 +1023,21 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
                 }
             }
         }
-        // ---- table: the visited lanes' positions (the last of a hash wins), then lane a's i+1
+        // ---- table: the visited lanes' positions (the last of a hash wins), then lane a's i+1.
+        // Lanes past the acceptor put back what their visit found (visits Go never makes); lane a+1
+        // hashed position i+1 itself and is the only lane past a that restores that entry, so it
+        // writes i+1 there instead when the acceptor makes the insert (prio bit 2; the acceptor
+        // still does it when a is the group's last lane)
+        const bool ins_next = TB != 0 && (prio & 4) && a >= 0 && a < G - 1 && ((sel >> 30) & 1);
         if (TB == 12) {
-            if (valid && a >= 0 && lj > a && cand <= i + a) lds_put12((uint64_t *)hth, h, (uint32_t)cand);
+            if (valid && a >= 0 && lj > a && cand <= i + a) lds_put12((uint64_t *)hth, h, (uint32_t)(ins_next && lj == a + 1 ? x : cand));
         } else if (TB == 16) {
-            if (valid && a >= 0 && lj > a && cand <= i + a) hth[h] = (uint16_t)cand;  // (visits Go never makes)
+            if (valid && a >= 0 && lj > a && cand <= i + a) hth[h] = (uint16_t)(ins_next && lj == a + 1 ? x : cand);
         } else {
             if (valid && (a < 0 || lj <= a)) hth[h] = (uint16_t)x;
         }
-        if (act && lj == a) {
-            if (!rl && !zr && x + 1 + 4 <= n) {
+        if (act && lj == a && !ins_next) {
+            if (ins1) {
                 const uint32_t h1 = ((uint32_t)(w0.hi >> 8) * kHashMul) >> hsh;
                 if (TB == 12) lds_put12((uint64_t *)hth, h1, (uint32_t)(x + 1));
                 else hth[h1] = (uint16_t)(x + 1);
@@ -1045,6 +1066,7 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
             __builtin_nontemporal_store(rv, rec + (uint32_t)(nrec & 1));
 #endif
         }
+        } while (__ballot(live) == lm && budget >= 0);
     }
 }
 
@@ -1973,7 +1995,9 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     const uint32_t w12 = (uint32_t)((2 * ((a.hs + 4) / 5) + 3) & ~3ll);  // u32 words of a 12-bit table
     const uint32_t stride = t12 ? w12 : split_stride<16, true>(a), tw = t12 ? w12 : split_table_words<true>(a);
     const uint64_t rcap = rec_cap(a);
-    static const int prio = knob("EZ_K1S_PRIO", 1);
+    // bit 0: s_setprio 3 on the chain up to the candidate loads; bit 2: the i+1 insert by lane a+1
+    // (EZ_K1S_NEXT1=0 (A/B): by the acceptor, with its own hash)
+    static const int prio = knob("EZ_K1S_PRIO", 1) | (knob("EZ_K1S_NEXT1", 1) ? 4 : 0);
     uint8_t *edge = (uint8_t *)(recs + a.count * rcap);
     // (the edge area's first 128 bytes: the dummy region of idle groups; its last 16: the edge-slot
     // counter and the stream queue)
@@ -1988,7 +2012,7 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     // A/B on one box) or 24; EZ_K1S_FW=24 (A/B)
     static const bool w40 = knob("EZ_K1S_FW", 40) == 40;
     // persistent groups (a stream queue); EZ_K1S_PERSIST=0 (A/B): one launch block per 4 streams
-    static const bool persist = knob("EZ_K1S_PERSIST", 1) != 0;
+    static const bool persist = knob("EZ_K1S_PERSIST", 0) != 0;
     const size_t lds = (size_t)stride * 4 * S + (lw && msk ? (size_t)kWinLdsBytes * S : 0) + pad;
     hipError_t e;
     if (lw && msk) {

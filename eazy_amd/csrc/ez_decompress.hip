@@ -325,7 +325,7 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     if (g_decompress_variant < 0) {
         const char *v = knob_str("EZ_K2");
         g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w'
-                               : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : 0));
+                               : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : (v && strcmp(v, "jump") == 0 ? 'j' : 0)));
     }
     const uint64_t exact_grid = a.count < 4096 ? a.count : 4096;
     // Slots under 64 KiB go to K2r's lane per stream; longer ones (C2, C4, the sweep's long streams) to

@@ -379,6 +379,21 @@ __device__ __forceinline__ void kj_piece(const DecompressArgs &A, const JWork &W
     JTok t = tk[a];
     uint32_t nxt = a + 1 < H.ntok ? tk[a + 1].dst : 0xffffffffu;
     const uint8_t *in = A.in + A.in_off[s];
+    if (n == 16 && p0 + 16 <= t.dst + t.L) {  // the 16 bytes inside one token (long literals, runs, zeros)
+        const uint32_t x = (uint32_t)(base + p0);
+        if (t.kd == 0) {
+            const uint8_t *y = in + t.src + (p0 - t.dst);
+            const V16 v = y + 16 <= A.in + A.in_off[A.count] ? ld16v(y) : ld_clamped(y, A.in, A.in + A.in_off[A.count]);
+            by[0] = (uint32_t)v.lo, by[1] = (uint32_t)(v.lo >> 32), by[2] = (uint32_t)v.hi, by[3] = (uint32_t)(v.hi >> 32);
+            for (uint32_t k = 0; k < 16; k++) pt[k] = x + k;
+        } else if (t.kd == kJCopy) {
+            for (uint32_t k = 0; k < 16; k++) pt[k] = x + k;
+        } else {
+            const uint32_t D = t.kd & ~kJCopy;
+            for (uint32_t k = 0; k < 16; k++) pt[k] = p0 + k >= D ? x + k - D : kJZero;
+        }
+        return;
+    }
     for (uint32_t k = 0; k < n; k++) {
         const uint32_t p = p0 + k;
         while (p >= nxt) {

@@ -64,7 +64,8 @@ def _run(tmp_path, mode, nproc=2):
     assert goff.tolist() == np.concatenate([[0], np.cumsum([len(w) for w in want])]).tolist()
     assert packed == b"".join(want), "gathered packing differs from the single-rank packing"
     spans = [tuple(map(int, x.split(":"))) for x in open(tmp_path / "ranges.txt").read().split()]
-    assert spans[0][0] == 0 and spans[1][0] == spans[0][1] and sum(n for _, n in spans) == len(packed)
+    assert spans[0][0] == 0 and sum(n for _, n in spans) == len(packed)
+    assert all(spans[k + 1][0] == spans[k][0] + spans[k][1] for k in range(len(spans) - 1))
 
 
 def test_two_rank_gloo_exchange(tmp_path):

@@ -490,5 +490,8 @@ def test_k2j_chip_wide_decode(cuda):
             o = out.cpu().numpy()
             for i, k in enumerate(batch):
                 want, err, _ = orc.decompress(ins[k], cap=scap[i])
+                if err == 2:  # the slot is too small: the status (ENOSPC, as the exact decoder's) is the result
+                    assert int(st[i]) == ez.ENOSPC
+                    continue
                 n = int(sz[i])
-                assert o[ooff[i] : ooff[i] + n].tobytes() == want[:n], (k, n)
+                assert int(st[i]) == err and o[ooff[i] : ooff[i] + n].tobytes() == want, (k, n)

@@ -561,8 +561,8 @@ def test_reader_whole_decode_matches_read_by_read(cuda):
         return bytes(out), errs
 
     clean = stream()
-    # 16 MiB of a short pattern with a few varied bytes: > 20x expansion
-    dense_parts = [(b"abcdefgh" * 65536)[: 1 << 19] + bytes([k]) * 64 for k in range(32)]
+    # 16 MiB of zero runs with a few other bytes: > 20x expansion (about 50,000x)
+    dense_parts = [bytes(1 << 19) + bytes([k + 1]) * 64 for k in range(32)]
     dense = stream(data=dense_parts)
     assert len(b"".join(dense_parts)) > 20 * len(dense)
     cases = {"clean": (clean, True, plain, 0), "header": (stream(hdr=True), True, plain, 0),
