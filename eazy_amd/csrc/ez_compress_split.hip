@@ -651,6 +651,7 @@ struct WinLds {
 };
 constexpr int32_t kWinLdsBytes = 144;
 
+
 // The 32 bytes y-8 .. y+23 by dword-aligned loads (dwordx4, dwordx4, dword from floor4(p + y - 8))
 // and v_alignbyte: a 16-byte load at a byte-unaligned address costs the L1 one access per dword it
 // touches, an aligned one a single access (tools/mb_ta.hip, L1-resident: 64 vs 16 ns per scattered

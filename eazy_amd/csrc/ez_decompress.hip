@@ -333,6 +333,21 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     // 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5) - / 7.0, 1 MiB (K2w 29.7) - / 14.4;
     // C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms).
     int v = a.force ? a.force : (g_decompress_variant != 0 ? g_decompress_variant : (a.max_out >= long_slot ? 't' : 'r'));
+    // A few long streams whose output is at least twice their input (copies, not literals) go to
+    // K2j: K2t gives each stream one wave and walks its copy chains round by round, K2j the whole
+    // chip (C4s, 64 x 4 MiB: K2t 93.7 ms, K2j 11.4 ms; a lone 16 MiB log stream 171 / 11.7 ms).
+    // Literal-heavy buckets stay on K2t (C4 fp32 0.149 / 1.86 ms, C4h 0.31 / 2.65 ms), and so do
+    // batches of more streams, whose chains K2t runs side by side (1,024 x 1 MiB: 12.9 / 58.8 ms).
+    if (v == 't' && !a.force && g_decompress_variant == 0 && a.count <= 256 && a.max_out >= ((uint64_t)256 << 10)) {
+        uint64_t ext[4] = {0, 0, 0, 0};  // (the offsets may be a view into a larger batch's: absolute)
+        if ((e = hipMemcpyAsync(&ext[0], a.in_off, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(&ext[1], a.in_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(&ext[2], a.out_off, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipMemcpyAsync(&ext[3], a.out_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        const uint64_t nin = ext[1] - ext[0], nout = ext[3] - ext[2];
+        if (nin >= (uint64_t)a.count * (64 << 10) && nout >= 2 * nin) v = 'j';
+    }
     if (v == 'j' && !jump_applies(a)) v = 't';
     g_last_variant = v;
     if (v == 'j') {

@@ -404,8 +404,9 @@ def test_k2t_deferred_literal_neighbours(cuda):
 @pytest.mark.gpu
 def test_decoder_routing_without_hint(cuda):
     """The batch decoder follows the largest output slot, measured on the device when the
-    caller gives no max_len: C4-class buckets (4 MiB) take K2t, 16 KiB and 4 KiB streams K2r,
-    each byte-exact against the input, with and without the hint."""
+    caller gives no max_len: C4-class buckets (4 MiB, literals) take K2t, a few long log streams
+    (output at least twice the input) K2j, 16 KiB and 4 KiB streams K2r, each byte-exact against
+    the input, with and without the hint."""
     import torch
 
     import eazy_amd as ez
@@ -413,6 +414,7 @@ def test_decoder_routing_without_hint(cuda):
 
     cases = [
         ([b.tobytes() for b in np.split(synth.f32(5, 4 * (1 << 20)).view(np.uint8), 4)], "t"),
+        ([synth.logs(40 + k, 1 << 20).tobytes() for k in range(4)], "j"),
         ([synth.logs(6 + k, 16 << 10).tobytes() for k in range(8)], "r"),
         ([synth.logs(20 + k, 4096).tobytes() for k in range(40)] + [b"", b"x" * 17], "r"),
     ]
