@@ -384,6 +384,8 @@ class Reader {
         p.resize(k);
         return {p, e};
     }
+    // the C-ABI handle (tests, measurement: ez_reader_whole_decoded, ez_reader_set_whole)
+    ez_reader *Handle() const { return h_; }
 
   private:
     ez_reader *h_ = nullptr;

@@ -713,6 +713,22 @@ extern "C" int ez_reader_whole_decoded(const ez_reader *r) { return r->ahead_on;
 extern "C" int ez_reader_pending(const ez_reader *r) { return r->st.state != 0 ? 1 : 0; }
 
 namespace {
+// K2j's workspace for Reader handles, one per device: a whole-stream decode is synchronous, so the
+// handles of a device take turns with it (a handle of its own would be allocated anew for every
+// NewReaderBytes, tens of ms for a large stream)
+struct ReaderJws {
+    std::mutex mu;
+    DBuf buf;
+};
+ReaderJws &reader_jws(int dev) {
+    static std::mutex m;
+    static std::map<int, ReaderJws *> all;
+    std::lock_guard<std::mutex> lk(m);
+    ReaderJws *&p = all[dev];
+    if (!p) p = new ReaderJws();
+    return *p;
+}
+
 constexpr size_t kAheadMax = ((size_t)1 << 30) - 64;  // the largest output slot (K2t takes slots below 2^30)
 constexpr size_t kAheadBrk = (size_t)1 << 16;         // Break positions recorded (more: Read by Read)
 constexpr size_t kStage = (size_t)4 << 20;            // the pinned staging window (host memory per Reader)
@@ -764,10 +780,20 @@ int reader_ahead(ez_reader *r, const uint8_t *b, size_t b_len) {
         a.max_out = cap;
         // one stream: K2j (chip-wide) for a long one, else the token-parallel wave
         a.force = b_len >= ((size_t)16 << 10) ? 'j' : 't';
-        if (ez::launch_decompress(a, r->stream) != hipSuccess) return 0;
-        if (hipMemcpyAsync(m, r->a_meta.p, sizeof m, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
-        if (hipMemcpyAsync(&nbrk, r->a_brk.p, 8, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
-        if (hipStreamSynchronize(r->stream) != hipSuccess) return 0;
+        {
+            ReaderJws &J = reader_jws(r->device);
+            std::lock_guard<std::mutex> lk(J.mu);
+            if (a.force == 'j') {
+                const uint64_t need = ez::jump_workspace_bytes(1, b_len, cap);
+                if (J.buf.ensure(need)) return 0;
+                a.jws = J.buf.p;
+                a.jws_cap = J.buf.cap;
+            }
+            if (ez::launch_decompress(a, r->stream) != hipSuccess) return 0;
+            if (hipMemcpyAsync(m, r->a_meta.p, sizeof m, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
+            if (hipMemcpyAsync(&nbrk, r->a_brk.p, 8, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
+            if (hipStreamSynchronize(r->stream) != hipSuccess) return 0;
+        }
         const int status = (int32_t)(m[5] & 0xffffffffu);
         if ((int64_t)m[6] == -2 && status == EZ_ENOSPC && cap < kAheadMax) {  // the slot was too small
             cap = cap < kAheadMax / 4 ? 4 * cap : kAheadMax;

@@ -338,7 +338,7 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     // chip (C4s, 64 x 4 MiB: K2t 93.7 ms, K2j 11.4 ms; a lone 16 MiB log stream 171 / 11.7 ms).
     // Literal-heavy buckets stay on K2t (C4 fp32 0.149 / 1.86 ms, C4h 0.31 / 2.65 ms), and so do
     // batches of more streams, whose chains K2t runs side by side (1,024 x 1 MiB: 12.9 / 58.8 ms).
-    if (v == 't' && !a.force && g_decompress_variant == 0 && a.count <= 256 && a.max_out >= ((uint64_t)256 << 10)) {
+    if (v == 't' && !a.force && g_decompress_variant == 0 && a.count <= 256 && a.max_out >= ((uint64_t)1 << 20)) {
         uint64_t ext[4] = {0, 0, 0, 0};  // (the offsets may be a view into a larger batch's: absolute)
         if ((e = hipMemcpyAsync(&ext[0], a.in_off, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipMemcpyAsync(&ext[1], a.in_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;

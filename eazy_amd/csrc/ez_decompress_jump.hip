@@ -527,10 +527,34 @@ std::map<std::pair<int, hipStream_t>, JScratch> g_jws;
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
+// the workspace layout of a batch (in_total / out_total: the end offsets in_off[count], out_off[count])
+struct JLayout {
+    uint64_t chunks, tok_cap;
+    size_t o_head, o_cbase, o_entry, o_sexit, o_bits, o_cnt, o_cout, o_cflag, o_ctb, o_cob, o_tok, o_ptr, o_pass, total;
+    JLayout(uint64_t count, uint64_t in_total, uint64_t out_total) {
+        chunks = in_total / kJC + 2 * count + 2;
+        tok_cap = in_total + 16;
+        size_t off = 0;
+        auto take = [&](size_t n) {
+            const size_t o = off;
+            off += al256(n);
+            return o;
+        };
+        o_head = take(sizeof(JHead) * count), o_cbase = take(4 * (count + 1)), o_entry = take(4 * chunks), o_sexit = take(4 * chunks),
+        o_bits = take(4 * kJW * chunks), o_cnt = take(4 * chunks), o_cout = take(8 * chunks), o_cflag = take(4 * chunks),
+        o_ctb = take(8 * chunks), o_cob = take(8 * chunks), o_tok = take(sizeof(JTok) * tok_cap), o_ptr = take(4 * out_total + 16),
+        o_pass = take(8 * (kJPasses + 2));
+        total = off;
+    }
+};
 }  // namespace
 
-// Streams K2j takes: a batch of at most kJMaxStreams streams (slots below 4 GiB in all)
+// Streams K2j takes: a batch of at most 1,024 streams (slots below 4 GiB in all)
 bool jump_applies(const DecompressArgs &a) { return a.count >= 1 && a.count <= 1024; }
+
+uint64_t jump_workspace_bytes(uint64_t count, uint64_t in_total, uint64_t out_total) {
+    return JLayout(count, in_total, out_total).total;
+}
 
 hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
     // the batch's input and output extents (one read back: the workspace is sized from them)
@@ -540,30 +564,29 @@ hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
     if ((e = hipMemcpyAsync(&ext[1], a.out_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
     const uint64_t in_total = ext[0], out_total = ext[1];
-    const uint64_t chunks = in_total / kJC + 2 * a.count + 2;
-    const uint64_t tok_cap = in_total + 16;
-    size_t off = 0;
-    auto take = [&](size_t n) {
-        const size_t o = off;
-        off += al256(n);
-        return o;
-    };
-    const size_t o_head = take(sizeof(JHead) * a.count), o_cbase = take(4 * (a.count + 1)), o_entry = take(4 * chunks),
-                 o_sexit = take(4 * chunks), o_bits = take(4 * kJW * chunks), o_cnt = take(4 * chunks), o_cout = take(8 * chunks),
-                 o_cflag = take(4 * chunks), o_ctb = take(8 * chunks), o_cob = take(8 * chunks), o_tok = take(sizeof(JTok) * tok_cap),
-                 o_ptr = take(4 * out_total + 16), o_pass = take(8 * (kJPasses + 2));
-    int dev = 0;
-    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-    std::lock_guard<std::mutex> lk(g_jmu);
-    JScratch &sc = g_jws[std::make_pair(dev, st)];
-    if (sc.cap < off) {
-        if (sc.p) (void)hipFree(sc.p);
-        sc.p = nullptr;
-        sc.cap = 0;
-        if ((e = hipMalloc(&sc.p, off + off / 4)) != hipSuccess) return e;
-        sc.cap = off + off / 4;
+    const JLayout Y(a.count, in_total, out_total);
+    const uint64_t chunks = Y.chunks, tok_cap = Y.tok_cap;
+    const size_t o_head = Y.o_head, o_cbase = Y.o_cbase, o_entry = Y.o_entry, o_sexit = Y.o_sexit, o_bits = Y.o_bits, o_cnt = Y.o_cnt,
+                 o_cout = Y.o_cout, o_cflag = Y.o_cflag, o_ctb = Y.o_ctb, o_cob = Y.o_cob, o_tok = Y.o_tok, o_ptr = Y.o_ptr,
+                 o_pass = Y.o_pass;
+    // the caller's workspace when it gives one large enough, else this (device, stream)'s (the lock
+    // is held through the launches: another host thread growing it meanwhile would free it under them)
+    std::unique_lock<std::mutex> lk(g_jmu, std::defer_lock);
+    uint8_t *w = (uint8_t *)a.jws;
+    if (!w || a.jws_cap < Y.total) {
+        int dev = 0;
+        if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+        lk.lock();
+        JScratch &sc = g_jws[std::make_pair(dev, st)];
+        if (sc.cap < Y.total) {
+            if (sc.p) (void)hipFree(sc.p);
+            sc.p = nullptr;
+            sc.cap = 0;
+            if ((e = hipMalloc(&sc.p, Y.total + Y.total / 4)) != hipSuccess) return e;
+            sc.cap = Y.total + Y.total / 4;
+        }
+        w = (uint8_t *)sc.p;
     }
-    uint8_t *w = (uint8_t *)sc.p;
     JWork W{};
     W.head = (JHead *)(w + o_head);
     W.cbase = (uint32_t *)(w + o_cbase);

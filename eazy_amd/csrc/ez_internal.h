@@ -118,6 +118,10 @@ struct DecompressArgs {
     uint64_t *breaks;
     uint64_t breaks_cap;
     int64_t *end_state;
+    // K2j's workspace, optional (jump_workspace_bytes): a synchronous caller (a Reader handle) passes
+    // one it owns; without it the launcher keeps one per (device, HIP stream)
+    void *jws;
+    uint64_t jws_cap;
     int force;                // batch: the first K2 kernel ('r', 't', ...; 0 = the automatic / selected one)
 };
 
@@ -161,6 +165,7 @@ hipError_t launch_defer_copy(const DecompressArgs &a, hipStream_t s);       // K
 // K2j (ez_decompress_jump.hip): batches of at most 1,024 streams, chip-wide token starts, token
 // records and pointer jumping over the copied bytes; streams it cannot take go to slow
 bool jump_applies(const DecompressArgs &a);
+uint64_t jump_workspace_bytes(uint64_t count, uint64_t in_total, uint64_t out_total);
 hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t s);
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t s);   // K2t, token-parallel wave per stream
 bool lds_exchange_in_lane_order();  // the LDS property K1s-T32 relies on (checked once)

@@ -4,6 +4,7 @@
 //
 //   ./eazy_test          all tests (needs an MI355X for the Writer/Reader ones)
 //   ./eazy_test --cpu    host-only tests: the token codec, compress bound, ABI
+#include <chrono>
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -584,6 +585,50 @@ static int dump_file(const char *path) {
     return 0;
 }
 
+// --perf-reader COMP PLAIN READ: NewReaderBytes(COMP) read to EOF with Read(READ bytes) through the
+// C++ mirror (the drop-in path without Python), checked against PLAIN; prints the rate and the time
+// of the first Read (the whole-stream decode)
+static std::vector<uint8_t> read_file(const char *path) {
+    std::vector<uint8_t> b;
+    FILE *f = std::fopen(path, "rb");
+    if (!f) return b;
+    uint8_t tmp[1 << 16];
+    size_t k;
+    while ((k = std::fread(tmp, 1, sizeof tmp, f)) > 0) b.insert(b.end(), tmp, tmp + k);
+    std::fclose(f);
+    return b;
+}
+static int perf_reader(const char *comp_path, const char *plain_path, size_t rs, int whole) {
+    const std::vector<uint8_t> comp = read_file(comp_path), plain = read_file(plain_path);
+    std::vector<uint8_t> got(plain.size() + rs), p(rs);
+    {  // (once per process: the HIP runtime's start and the device's decode workspace, by a first Reader
+        // over the same stream; the timed one is a fresh handle)
+        auto w = NewReaderBytes(comp);
+        std::vector<uint8_t> q(4096);
+        (void)w->Read(q.data(), q.size());
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    auto r = NewReaderBytes(comp);
+    if (!whole) ez_reader_set_whole(r->Handle(), 0);
+    size_t at = 0;
+    double first = -1;
+    Err e = Err::OK;
+    for (;;) {
+        auto [n, err] = r->Read(p.data(), rs);
+        if (first < 0) first = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        if (at + n > got.size()) return 3;
+        std::memcpy(got.data() + at, p.data(), n);
+        at += n;
+        e = err;
+        if (err != Err::OK) break;
+    }
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const bool ok = e == Err::EOF_ && at == plain.size() && std::memcmp(got.data(), plain.data(), at) == 0;
+    std::printf("{\"reader\": \"%s\", \"read_bytes\": %zu, \"MiBps\": %.1f, \"first_read_ms\": %.2f, \"ok\": %s}\n",
+                whole ? "whole" : "read_by_read", rs, (double)at / t / 1048576.0, first * 1e3, ok ? "true" : "false");
+    return ok ? 0 : 1;
+}
+
 // Dumper::ReadFrom with the stream in one read prints what one Write prints, and a stream cut
 // inside a token ends in UnexpectedEOF (reader.go:563-600).  (Reads that cut a token do not
 // print what Dump prints: like the reference, Write reports the bytes up to the cut token's
@@ -629,6 +674,7 @@ static void TestDumperReadFrom() {
 
 int main(int argc, char **argv) {
     if (argc > 2 && std::string(argv[1]) == "--dump") return dump_file(argv[2]);
+    if (argc > 5 && std::string(argv[1]) == "--perf-reader") return perf_reader(argv[2], argv[3], (size_t)std::atol(argv[4]), std::atoi(argv[5]));
     const bool cpu = argc > 1 && std::string(argv[1]) == "--cpu";
     run("TestPrintLengthEncoding", TestPrintLengthEncoding);
     run("TestPrintOffsetEncoding", TestPrintOffsetEncoding);

@@ -114,6 +114,24 @@ def main():
     t0 = time.perf_counter()
     assert orc.decompress(comp, 4096)[0] == plain
     rd["cpu_oracle_read4k_MiBps"] = len(plain) / (time.perf_counter() - t0) / 2**20
+    # the same Read(4 KiB) loops through the C++ mirror (eazy_amd/cpp/eazy.hpp): the drop-in path
+    # without the Python layer's per-call cost
+    import subprocess
+    import tempfile
+
+    exe = os.path.join(ROOT, "tests", "cpp", "eazy_test")
+    if os.path.exists(exe):
+        with tempfile.TemporaryDirectory() as d:
+            cf, pf = os.path.join(d, "c.bin"), os.path.join(d, "p.bin")
+            open(cf, "wb").write(comp)
+            open(pf, "wb").write(plain)
+            for whole in (1, 0):
+                p = subprocess.run([exe, "--perf-reader", cf, pf, "4096", str(whole)], capture_output=True, text=True, timeout=300)
+                line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+                if p.returncode == 0 and line:
+                    j = json.loads(line[0])
+                    rd[f"cpp_{j['reader']}_MiBps"] = j["MiBps"]
+                    rd[f"cpp_{j['reader']}_first_read_ms"] = j["first_read_ms"]
     print(json.dumps({"handle_path": res, "writes_per_size": a.writes, "reader_16MiB_read4k": rd,
                       "note": "ez_writer_write per call: one pinned H2D copy, the general kernel (a wave), one D2H copy, one sync; "
                               "batch64: ez_writer_write_batch of 64 Writes per call"}))
