@@ -181,6 +181,15 @@ def decompress_kernel_last() -> str:
     return chr(v) if v else ""
 
 
+def k1c_stats(enable: bool) -> dict:
+    """K1c's verdict counts so far (streams proven; fallen back to K1L for a chunk error or
+    re-visit, no common copy end, a changed judgement, the record slot; path segments), then
+    counting on (cleared) or off.  While on, each K1c batch waits for its verdicts.  Tests only."""
+    out = (C.c_uint64 * 6)()
+    _check(_lib().ez_compress_k1c_stats(1 if enable else 0, out))
+    return dict(zip(("proven", "chunk", "sync", "judge", "cap", "segments"), (int(v) for v in out)))
+
+
 def _check(code: int, detail: int = 0) -> None:
     if code == OK:
         return

@@ -1074,6 +1074,11 @@ extern "C" int ez_select_decompress_kernel(int kind) {
 
 extern "C" int ez_decompress_kernel_last(void) { return ez::last_decompress_variant(); }
 
+extern "C" int ez_compress_k1c_stats(int enable, uint64_t *counts) {
+    ez::k1c_stats(enable, counts);
+    return EZ_OK;
+}
+
 extern "C" size_t ez_decompress_workspace(uint64_t count) {
     return (size_t)ez::decompress_workspace_words(count) * sizeof(uint32_t);
 }

@@ -729,6 +729,7 @@ char compress_variant(const CompressArgs &a) {
 }
 
 bool compress_forced_general() { return forced_variant() == 'w'; }
+bool compress_forced_long() { return forced_variant() == 'l'; }
 
 hipError_t launch_compress(const CompressArgs &a, hipStream_t st) {
     if (a.count == 0) return hipSuccess;

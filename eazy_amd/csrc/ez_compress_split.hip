@@ -45,7 +45,9 @@
 #include "ez_wave.h"
 #include "ez_k1_common.h"
 
+#include <cstdio>
 #include <type_traits>
+#include <vector>
 
 #ifndef EZ_EXP
 #define EZ_EXP 0  // diagnostic builds only: bit 2 = cycle profile of the parse loop
@@ -1360,6 +1362,7 @@ struct RingSrc {
 // the Write); the window's bytes and the candidates' come from there, anything else from RingSrc.
 constexpr int32_t kLdsRing = 32768, kLdsWrite = 49152;
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
+typedef uint32_t __attribute__((aligned(1))) u32_ua;
 struct LdsSrc {
     const uint8_t *lds;
     int32_t rl, n;
@@ -1408,13 +1411,20 @@ struct WindowFromSrc<LdsSrc> {
 // per SIMD), and at C2 one accepted copy in nine is 24 - 39 bytes long, whose exact extension
 // (gext_long) is a group-wide round trip that every stream of the wave waits for.
 constexpr int32_t kLCap = 40;
-template <class SRC, bool LW = false>
+// K1c's side outputs of a chunk's speculative parse (see kc_parse); NoEv: none (K1L)
+struct NoEv {
+    static constexpr bool kOn = false;
+    int32_t stop, keep;
+    uint32_t cnt;
+    __device__ __forceinline__ void visit(int32_t, int32_t, bool, bool, int, int, int32_t, bool, int32_t) {}
+};
+template <class SRC, bool LW = false, class EV = NoEv>
 __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_t n, int32_t i, int32_t done, int64_t bs, int lj,
                                           int g, uint32_t *htw, uint32_t hsh, uint4 *rec, uint64_t rcap, const uint8_t *blo,
-                                          const uint8_t *bhi, int32_t &nrec_out, int &err, uint8_t *wl = nullptr) {
+                                          const uint8_t *bhi, int32_t &nrec_out, int &err, uint8_t *wl = nullptr, EV *ev = nullptr) {
     constexpr int G = 16;
     int32_t nrec = 0;
-    bool live = !err && i + 4 <= n;
+    bool live = !err && i + 4 <= n && (!EV::kOn || i < ev->stop);
     int64_t guard = 4 * (int64_t)n + 64;
     V16 w0{0, 0}, w1{0, 0}, w2{0, 0};  // bytes x-8 .. x+7, x+8 .. x+23, x+24 .. x+39 of this lane's position x
     typename std::conditional<LW, WinLdsL, WinRollL>::type wr;
@@ -1534,23 +1544,35 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
             }
         }
         EZ_PROF_MARK(4);
+        // K1c: the window's visits (and the i+1 insert) into the chunk's log, in the parse's order
+        bool keep = true;
+        uint32_t logi = 0;
+        if constexpr (EV::kOn) {
+            const bool insb = bcast((int32_t)(act && lj == a && !rl && !zr && x + 1 + 4 <= n), al) != 0;
+            ev->visit(x, cand, valid && (a < 0 || lj <= a), act && lj == a, g, lj, i, insb, i + (a < 0 ? 0 : a) + 1);
+            logi = ev->cnt;
+            keep = nxt >= ev->keep;
+        }
         // ---- table: the visited lanes' positions (the last of a hash wins), then lane a's i+1
         if (valid && (a < 0 || lj <= a)) htw[h] = (uint32_t)x;
         if (act && lj == a) {
             if (!rl && !zr && x + 1 + 4 <= n) htw[((uint32_t)(w0.hi >> 8) * kHashMul) >> hsh] = (uint32_t)(x + 1);
         }
         // the record, stored after the next region's load is issued (as in lean_loop)
-        const bool st_rec = act && lj == a && (uint64_t)nrec < rcap;
-        const u32x4 recv{(uint32_t)lit, (uint32_t)(nx - lit), (uint32_t)dist, force ? 1u : 0u};
+        const bool st_rec = act && lj == a && keep && (uint64_t)nrec < rcap;
+        // (K1c: the log's length after this window in the flags word's bits 1..31; k1_emit reads bit 0)
+        const u32x4 recv{(uint32_t)lit, (uint32_t)(nx - lit), (uint32_t)dist, (force ? 1u : 0u) | (logi << 1)};
         u32x4 *const recp = (u32x4 *)(rec + nrec);
         if (act) {
-            if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
-            nrec++;
+            if (keep) {
+                if ((uint64_t)nrec >= rcap) { err = EZ_ESTUCK; live = false; }
+                nrec++;
+            }
             i = done = nxt;
         } else if (live) {
             i += nvalid;
         }
-        if (live && (err || i + 4 > n)) live = false;
+        if (live && (err || i + 4 > n || (EV::kOn && i >= ev->stop))) live = false;
         if (!kWinSrc) wr.advance(p, i, lj, live, blo, bhi);  // the next window's region
         __builtin_amdgcn_sched_barrier(0);
         if (st_rec) __builtin_nontemporal_store(recv, recp);
@@ -1568,8 +1590,10 @@ __device__ __forceinline__ void long_loop(const SRC &P, const uint8_t *p, int32_
 // a group of 16 lanes per stream, 4 streams per wave; spec_mode 2: K1x's streams resume
 // spw: streams per wave (1, 2 or 4; the other lane groups idle, with no table): a batch of few long
 // streams runs more waves per SIMD, each a lone latency chain, instead of fewer waves of 4 streams
+// only (K1c's fallback): the streams whose only[ostride s] is nonzero, the others untouched (nullptr: all)
 template <bool LW = false>
-__global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_words, uint4 *recs, uint64_t rcap, uint32_t spw) {
+__global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_words, uint4 *recs, uint64_t rcap, uint32_t spw,
+                                              const uint32_t *only, uint32_t ostride) {
     constexpr int G = 16;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = (int)(threadIdx.x & 63);
@@ -1581,6 +1605,7 @@ __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_wor
     const bool spec = A.spec_mode != 0;
     bool have = grp && s < A.count;
     if (have && spec && A.spec[s].flags != 0) have = false;  // finished by K1x
+    if (have && only && only[(uint64_t)ostride * s] == 0) have = false;  // K1c took it
     const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
     int32_t n = 0, i = 0, done = 0;
     const uint8_t *p = blo;
@@ -1601,6 +1626,402 @@ __global__ __launch_bounds__(64) void k1_long(CompressArgs A, uint32_t table_wor
     long_loop<FreshSrc, LW>(FreshSrc{{p, blo, bhi}}, p, n, i, done, A.bs, lj, g, htw, hsh, recs + (have ? s * rcap : 0), rcap, blo, bhi,
                             nrec, err, wl);
     if (have && lj == 0) A.out_size[s] = (uint64_t)nrec | ((uint64_t)err << 48);
+}
+
+// ---------------------------------------------------------------- K1c: chunk-parallel long streams
+// K1L runs one 16-lane group per stream: a batch of few long streams (C2's 4,096 x 256 KiB: one wave
+// per SIMD; C4s's 64 streams after K1x) leaves the chip waiting on a few dependent chains.  K1c cuts
+// each stream into chunks of C positions and parses all of them at once, then proves the result is
+// Go's parse (writer.go:206-330) or hands the stream to K1L:
+//   kc_parse   chunk k's speculative parse (long_loop): from W positions before its start b_k with
+//              done there and a zero table, to O positions past the next chunk's start.  It keeps the
+//              records ending at or after b_k and logs its visits in the order it makes them -- the
+//              position and the table entry it read (bit 31: it accepted there), an i+1 insert as a
+//              marker -- each record carrying the log's length after its window.  Chunk 0 starts where
+//              the stream does (or at K1x's state), so its parse is Go's up to where it stops.
+//   kc_stitch  per stream: the path is chunk 0's parse up to the first copy end it shares with chunk
+//              1's parse (i == done == that position in both: from there the two make the same
+//              choices as long as they read the same table entries), then chunk 1's, and so on (past
+//              a copy over the next chunk's start: the first later chunk that ends a copy at one of
+//              this one's copy ends).  A segment = (chunk, its records and its log range).
+//   kc_gather  the path's records into the stream's record slot (K1L's layout, for k1_emit<true>).
+//   kc_v1/v2   every logged read against the table of the stitched path itself (Go's table at that
+//              visit: the last position of that hash visited or inserted before it in the path's
+//              order; 0 at the stream start, K1x's table after its rounds): kc_v1 per segment with an
+//              LDS table, kc_v2 per hash across segments for each segment's first read of it.  A visit
+//              that read another entry is judged again with the right one and the path's pending
+//              literal start (kc_accepts, long_loop's judgement): still a reject, the path stands (the
+//              entry read decides only that visit; the table holds positions, not what was read); an
+//              accept, or an acceptor that read another entry, fails the stream.
+// Every choice of the stitched path is then Go's choice from Go's state, so it is Go's parse.
+// Passes: a chunk's zero table at its warm-up misses entries older than the warm-up, and a visit that
+// would have accepted with one fails the stream; the next pass parses again each chunk whose segment
+// failed, from that segment's start (i == done there) with the stitched path's table at that point
+// (kc_v2 writes both), which is Go's when the path before it is -- so each pass proves at least the
+// first failed segment, and in practice most of them (the others keep their parses; every segment is
+// checked again against the new path).  Streams still
+// failed after the last pass, or that cannot be stitched (a chunk's error or log overflow, no shared
+// copy end), take K1L from their start (k1_long's `only`).
+struct KcBufs {
+    uint4 *crec;      // per chunk: rcap_c records (K1L's; flags word bit 1..: the log length)
+    uint2 *log;       // per chunk: logcap visits {position, entry read | accept << 31, or kKcIns}
+    uint4 *meta;      // per chunk: {records kept, flags kKc*, log length, 0}
+    uint32_t *seg;    // per stream: kmax segments of 8 words {chunk, from, to, rec lo, rec hi, rec dst, log lo, log hi}
+    uint32_t *sinfo;  // per stream: kKcInfo words {segments, fail, chunks, first failed segment, pass}
+    uint32_t *ft;     // per segment: first read's log index [hs], last position [hs]
+    int32_t *cstart;  // per chunk: the next pass's start (a segment's start; -1: the warm-up start)
+    uint32_t *t0;     // per chunk: the next pass's table at that start [hs]
+    uint32_t *cfail;  // per chunk: its segment failed a check this pass (the next pass parses it again)
+    int32_t C, W, O, kmax, logcap;
+    uint32_t rcap_c;
+};
+constexpr uint32_t kKcHave = 1, kKcErr = 2, kKcBad = 4, kKcLast = 8;
+constexpr uint32_t kKcIns = 0xfffffffeu, kKcNone = 0xffffffffu;
+// fail codes (sinfo[3 s + 1]): a chunk's error or log overflow, no shared copy end, a judgement
+// changed, the record slot
+constexpr uint32_t kKcFailChunk = 1, kKcFailSync = 2, kKcFailJudge = 4, kKcFailCap = 8;
+constexpr int kKcSegWords = 8, kKcInfo = 5;
+
+struct ChunkEv {
+    static constexpr bool kOn = true;
+    int32_t stop, keep;
+    uint32_t cnt;
+    int bad;
+    int32_t base;
+    uint32_t cap;
+    uint2 *log;
+    // the window's visits (lanes 0 .. a, or all valid lanes) and the acceptor's i+1 insert
+    // (group-uniform); windows wholly before the chunk are not logged (no segment reaches them)
+    __device__ __forceinline__ void visit(int32_t x, int32_t cand, bool vis, bool acc, int g, int lj, int32_t i, bool insb,
+                                          int32_t x1) {
+        if (i + 16 <= base || bad) return;
+        const uint32_t vm = gball<16>(vis, g);
+        const uint32_t nv = (uint32_t)__builtin_popcount(vm);
+        if (cnt + nv + 1 > cap) {
+            bad = 1;
+            return;
+        }
+        if (vis) log[cnt + (uint32_t)lj] = make_uint2((uint32_t)x, (uint32_t)cand | (acc ? 0x80000000u : 0u));
+        if (insb && lj == 0) log[cnt + nv] = make_uint2((uint32_t)x1, kKcIns);
+        cnt += nv + (insb ? 1u : 0u);
+    }
+};
+
+template <bool LW>
+__global__ __launch_bounds__(64) void kc_parse(CompressArgs A, KcBufs B, int pass) {
+    constexpr int G = 16;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = (int)(threadIdx.x & 63);
+    const int g = lane / G, lj = lane % G;
+    const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(A.hs - 1)));
+    uint32_t *htw = (uint32_t *)smem + (uint32_t)g * (uint32_t)A.hs;
+    const uint64_t c = (uint64_t)blockIdx.x * 4 + (uint32_t)g;
+    const uint64_t s = c / (uint64_t)B.kmax;
+    const int32_t k = (int32_t)(c % (uint64_t)B.kmax);
+    const bool spec = A.spec_mode != 0;
+    bool have = s < A.count;
+    if (have && spec && A.spec[s].flags != 0) have = false;
+    const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
+    int32_t n = 0, from0 = 0, done0 = 0;
+    const uint8_t *p = blo;
+    if (have) {
+        n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+        p = A.in + A.in_off[s];
+        if (spec) {
+            from0 = (int32_t)A.spec[s].from;
+            done0 = (int32_t)A.spec[s].done;
+        }
+    }
+    const int64_t b = (int64_t)from0 + (int64_t)k * B.C;
+    if (have && k > 0 && b + 4 > n) have = false;  // no such chunk
+    // later passes: the streams the last one failed on a judgement, from the failed segment's chunk on
+    bool touch = have;
+    int32_t cs = -1;
+    if (have && pass > 1) {
+        if (B.sinfo[kKcInfo * s + 1] != kKcFailJudge || B.cfail[c] == 0) touch = have = false;
+        else cs = B.cstart[c];
+    }
+    const bool last = have && b + B.C + 4 > n;
+    int32_t i0 = k == 0 ? from0 : (int32_t)(b - B.W > from0 ? b - B.W : from0);
+    int32_t d0 = k == 0 ? done0 : i0;
+    const uint32_t *tsrc = nullptr;
+    if (cs >= 0) {  // a segment's start in the last pass's path, with its table there
+        i0 = d0 = cs;
+        tsrc = B.t0 + c * (uint64_t)A.hs;
+    } else if (have && k == 0 && spec) {
+        tsrc = A.spec_tab + s * (uint64_t)A.hs;
+    }
+    for (int32_t t = lj; t < (int32_t)A.hs; t += G) htw[t] = tsrc ? tsrc[t] : 0u;
+    ChunkEv ev;
+    ev.stop = last ? n : (int32_t)(b + B.C + B.O < n ? b + B.C + B.O : n);
+    ev.keep = k == 0 ? (int32_t)0x80000000 : (int32_t)b;
+    ev.cnt = 0;
+    ev.bad = 0;
+    ev.base = (int32_t)b;
+    ev.cap = (uint32_t)B.logcap;
+    ev.log = B.log + (have ? c : 0) * (uint64_t)B.logcap;
+    int err = have && (uint64_t)n > A.max_len ? EZ_EINVAL : (have ? 0 : EZ_EINVAL);
+    int32_t nrec = 0;
+    uint8_t *wl = smem + (size_t)4 * A.hs * 4 + (size_t)g * kWinLdsBytes;
+    long_loop<FreshSrc, LW, ChunkEv>(FreshSrc{{p, blo, bhi}}, p, n, have ? i0 : 0, have ? d0 : 0, A.bs, lj, g, htw, hsh,
+                                     B.crec + (have ? c : 0) * (uint64_t)B.rcap_c, B.rcap_c, blo, bhi, nrec, err, wl, &ev);
+    // (a start at a segment's start is a copy end of this parse too: the stitch may switch there)
+    if (lj == 0 && s < A.count && (pass == 1 || touch))
+        B.meta[c] = make_uint4((uint32_t)nrec, have ? (kKcHave | (err ? kKcErr : 0u) | (ev.bad ? kKcBad : 0u) | (last ? kKcLast : 0u)) : 0u,
+                               ev.cnt, cs >= 0 && cs >= b ? (uint32_t)cs : kKcNone);
+}
+
+__device__ __forceinline__ int32_t kc_nx(const uint4 &r) { return (int32_t)(r.x + r.y); }
+__device__ __forceinline__ uint32_t kc_li(const uint4 &r) { return r.w >> 1; }
+
+// the first record of r[lo, hi) ending at or after y (copy ends never decrease along a parse)
+__device__ __forceinline__ uint32_t kc_lower(const uint4 *r, uint32_t lo, uint32_t hi, int32_t y) {
+    while (lo < hi) {
+        const uint32_t m = lo + (hi - lo) / 2;
+        if (kc_nx(r[m]) < y) lo = m + 1;
+        else hi = m;
+    }
+    return lo;
+}
+
+// a thread per stream
+__global__ __launch_bounds__(64) void kc_stitch(CompressArgs A, KcBufs B, uint64_t rcap, int pass) {
+    const uint64_t s = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+    if (s >= A.count) return;
+    if (A.spec_mode != 0 && A.spec[s].flags != 0) return;
+    uint32_t *si = B.sinfo + kKcInfo * s;
+    if (pass > 1 && si[1] != kKcFailJudge) return;
+    const uint64_t c0 = s * (uint64_t)B.kmax;
+    const int32_t n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+    const int32_t from0 = A.spec_mode != 0 ? (int32_t)A.spec[s].from : 0;
+    uint32_t fail = 0;
+    int32_t K = 0;
+    for (int32_t k = 0; k < B.kmax; k++) {
+        const uint4 m = B.meta[c0 + k];
+        if (!(m.y & kKcHave)) break;
+        if (m.y & (kKcErr | kKcBad)) fail = kKcFailChunk;
+        K++;
+        if (m.y & kKcLast) break;
+    }
+    uint32_t *seg = B.seg + s * (uint64_t)B.kmax * kKcSegWords;
+    int32_t nseg = 0;
+    uint32_t tot = 0, ri = 0, li = 0;
+    int32_t o = 0, q = from0;
+    while (!fail && K > 0) {
+        const uint4 mo = B.meta[c0 + o];
+        const uint32_t no = mo.x;
+        const uint4 *ro = B.crec + (c0 + o) * (uint64_t)B.rcap_c;
+        uint32_t *e = seg + kKcSegWords * nseg;
+        if (o == K - 1) {
+            e[0] = (uint32_t)o, e[1] = (uint32_t)q, e[2] = (uint32_t)n, e[3] = ri, e[4] = no, e[5] = tot, e[6] = li, e[7] = mo.z;
+            nseg++;
+            tot += no - ri;
+            break;
+        }
+        const int32_t xl = no > ri ? kc_nx(ro[no - 1]) : -1;  // this parse's last copy end
+        bool found = false;
+        uint32_t fa = 0, fb = 0;
+        int32_t fj = 0, Q = 0;
+        bool virt = false;
+        for (int32_t j = o + 1; j < K && !found && (int64_t)from0 + (int64_t)j * B.C <= xl; j++) {
+            const int32_t bj = (int32_t)((int64_t)from0 + (int64_t)j * B.C);
+            const uint4 mj = B.meta[c0 + j];
+            const uint32_t nj = mj.x;
+            const uint4 *rj = B.crec + (c0 + j) * (uint64_t)B.rcap_c;
+            if (mj.w != kKcNone) {  // chunk j starts at a copy end of the last pass's path
+                const uint32_t ia = kc_lower(ro, ri, no, (int32_t)mj.w);
+                if (ia < no && kc_nx(ro[ia]) == (int32_t)mj.w) {
+                    found = virt = true;
+                    fa = ia, fj = j, Q = (int32_t)mj.w;
+                    break;
+                }
+            }
+            uint32_t ia = kc_lower(ro, ri, no, bj), ib = 0;
+            while (ia < no && ib < nj) {
+                const int32_t va = kc_nx(ro[ia]), vb = kc_nx(rj[ib]);
+                if (va == vb) {
+                    found = true;
+                    fa = ia, fb = ib, fj = j, Q = va;
+                    break;
+                }
+                if (va < vb) ia++;
+                else ib++;
+            }
+        }
+        if (!found) {
+            fail = kKcFailSync;
+            break;
+        }
+        e[0] = (uint32_t)o, e[1] = (uint32_t)q, e[2] = (uint32_t)Q, e[3] = ri, e[4] = fa + 1, e[5] = tot, e[6] = li, e[7] = kc_li(ro[fa]);
+        nseg++;
+        tot += fa + 1 - ri;
+        const uint4 *rj = B.crec + (c0 + fj) * (uint64_t)B.rcap_c;
+        li = virt ? 0u : kc_li(rj[fb]);
+        o = fj, q = Q, ri = virt ? 0u : fb + 1;
+    }
+    if (!fail && tot > rcap) fail = kKcFailCap;
+    si[0] = (uint32_t)nseg;
+    si[1] = fail;
+    si[2] = (uint32_t)K;
+    si[3] = kKcNone;
+    si[4] = (uint32_t)pass;
+    for (int32_t k = 0; k < K; k++) B.cstart[c0 + k] = -1, B.cfail[c0 + k] = 0;  // (kc_v2 sets the segments' owners)
+    if (!fail) A.out_size[s] = tot;
+}
+
+// streams still failed on a judgement after this pass (the host stops the passes at 0)
+__global__ __launch_bounds__(256) void kc_count(CompressArgs A, KcBufs B, uint32_t *left) {
+    const uint64_t s = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const bool f = s < A.count && !(A.spec_mode != 0 && A.spec[s].flags != 0) && B.sinfo[kKcInfo * s + 1] == kKcFailJudge;
+    const uint64_t m = __ballot(f);
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(left, (uint32_t)__builtin_popcountll(m));
+}
+
+// this pass's path of stream s is to be checked (stitched now, not given up)
+__device__ __forceinline__ bool kc_checking(const KcBufs &B, uint64_t s, int pass) {
+    const uint32_t *si = B.sinfo + kKcInfo * s;
+    return si[4] == (uint32_t)pass && (si[1] == 0 || si[1] == kKcFailJudge) && si[0] != 0;
+}
+
+// a block per (stream, segment): the segment's records into the stream's slot
+__global__ __launch_bounds__(256) void kc_gather(CompressArgs A, KcBufs B, uint4 *recs, uint64_t rcap, int pass) {
+    const uint64_t s = blockIdx.x / (uint32_t)B.kmax;
+    const uint32_t t = blockIdx.x % (uint32_t)B.kmax;
+    if (s >= A.count || (A.spec_mode != 0 && A.spec[s].flags != 0)) return;
+    if (!kc_checking(B, s, pass) || t >= B.sinfo[kKcInfo * s]) return;
+    const uint32_t *e = B.seg + (s * (uint64_t)B.kmax + t) * kKcSegWords;
+    const uint4 *src = B.crec + (s * (uint64_t)B.kmax + e[0]) * (uint64_t)B.rcap_c;
+    uint4 *dst = recs + s * rcap + e[5];
+    for (uint32_t r = e[3] + threadIdx.x; r < e[4]; r += 256) dst[r - e[3]] = src[r];
+}
+
+// Go's acceptance of position x with candidate cand while the pending literal starts at done: the
+// judgement of one lane of long_loop (writer.go:213-301, :441-473), from the stream's bytes
+__device__ bool kc_accepts(const uint8_t *p, int32_t n, int32_t x, int32_t cand, int32_t done, int64_t bs, const uint8_t *blo,
+                           const uint8_t *bhi) {
+    const FreshSrc P{{p, blo, bhi}};
+    const bool rl = cand >= done && cand < x;
+    if (!rl && (int64_t)done - cand > bs) return false;  // the far skip
+    V16 w0, w1, w2, c0, c1, c2;
+    bytes48_chk(p, x, w0, w1, w2, blo, bhi);
+    P.bytes48(cand, c0, c1, c2);
+    if (!rl && (int64_t)cand - 8 < (int64_t)done - bs) c0.lo = ring16(P, cand - 8, done, bs).lo;
+    int32_t jf = first_diff40(w0.hi ^ c0.hi, w1.lo ^ c1.lo, w1.hi ^ c1.hi, w2.lo ^ c2.lo, w2.hi ^ c2.hi);
+    jf = jf < n - x ? jf : n - x;
+    int32_t bl = x - done;
+    if (rl) bl = bl < cand ? bl : cand;
+    int32_t jb = last_diff8(w0.lo ^ c0.lo);
+    jb = jb < bl ? jb : bl;
+    const bool zr = rl && c0.hi == 0 && cand + 8 < n;
+    const int32_t fw = rl ? jf : (jf < done - cand ? jf : done - cand);
+    const int64_t t1 = bs - (int64_t)(x - cand);
+    const int32_t len = rl ? fw + jb : (int32_t)((int64_t)(fw + jb) < t1 ? (int64_t)(fw + jb) : (t1 < 0 ? -1 : t1));
+    return zr || len >= kMinCopyChunk;
+}
+
+// log entry li of segment e (stream s) read `got` (bit 31: it accepted) where the path's table held
+// `exact`: the stream stands only if that visit rejects with `exact` too, from the path's pending
+// literal start there (the last record of the segment logged before the visit, else the segment's start)
+__device__ void kc_recheck(const CompressArgs &A, const KcBufs &B, uint64_t s, uint32_t t, const uint32_t *e, uint32_t li,
+                           uint32_t got, uint32_t exact) {
+    bool bad = (got >> 31) != 0;
+    if (!bad) {
+        const uint4 *r = B.crec + (s * (uint64_t)B.kmax + e[0]) * (uint64_t)B.rcap_c;
+        uint32_t lo = e[3], hi = e[4];  // the first record logged after li
+        while (lo < hi) {
+            const uint32_t m = lo + (hi - lo) / 2;
+            if (kc_li(r[m]) <= li) lo = m + 1;
+            else hi = m;
+        }
+        const int32_t done = lo > e[3] ? kc_nx(r[lo - 1]) : (int32_t)e[1];
+        const int32_t x = (int32_t)B.log[(s * (uint64_t)B.kmax + e[0]) * (uint64_t)B.logcap + li].x;
+        const uint8_t *p = A.in + A.in_off[s];
+        const int32_t n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+        bad = kc_accepts(p, n, x, (int32_t)exact, done, A.bs, A.in, A.in + A.in_off[A.count]);
+    }
+    if (bad) {
+        B.sinfo[kKcInfo * s + 1] = kKcFailJudge;
+        atomicMin(B.sinfo + kKcInfo * s + 3, t);
+        B.cfail[s * (uint64_t)B.kmax + e[0]] = 1;
+    }
+}
+
+// a wave per (stream, segment): the segment's log in order, 64 visits a step; a visit's right entry
+// is the position of the nearest earlier same-hash event of the step (ballots over the hash bits)
+// or the segment's table so far; a segment's first read of a hash is left to kc_v2
+__global__ __launch_bounds__(64) void kc_v1(CompressArgs A, KcBufs B, int pass) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    uint32_t *T = (uint32_t *)smem, *F = T + A.hs;
+    const int lane = (int)threadIdx.x;
+    const uint64_t s = blockIdx.x / (uint32_t)B.kmax;
+    const uint32_t t = blockIdx.x % (uint32_t)B.kmax;
+    if (s >= A.count || (A.spec_mode != 0 && A.spec[s].flags != 0)) return;
+    if (!kc_checking(B, s, pass) || t >= B.sinfo[kKcInfo * s]) return;
+    const int32_t hs = (int32_t)A.hs;
+    const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(hs - 1)));
+    const int hb = 32 - (int)hsh;
+    for (int32_t u = lane; u < hs; u += 64) T[u] = F[u] = kKcNone;
+    const uint8_t *p = A.in + A.in_off[s];
+    const uint32_t *e = B.seg + (s * (uint64_t)B.kmax + t) * kKcSegWords;
+    const uint2 *lg = B.log + (s * (uint64_t)B.kmax + e[0]) * (uint64_t)B.logcap;
+    const uint32_t lhi = e[7];
+    __syncthreads();
+    for (uint32_t l0 = e[6]; l0 < lhi; l0 += 64) {
+        const uint32_t li = l0 + (uint32_t)lane;
+        const bool in = li < lhi;
+        const uint2 v = in ? lg[li] : make_uint2(0, 0);
+        const uint32_t h = in ? ((*(const u32_ua *)(p + v.x)) * kHashMul) >> hsh : 0u;
+        uint64_t m = __ballot(in);
+        for (int u = 0; u < hb; u++) {
+            const uint64_t bb = __ballot(in && ((h >> u) & 1));
+            m &= ((h >> u) & 1) ? bb : ~bb;
+        }
+        const uint64_t lower = lane == 0 ? 0ull : (m & (~0ull >> (64 - lane)));
+        const int pl = lower ? 63 - (int)__builtin_clzll(lower) : 0;
+        const uint32_t xp = (uint32_t)__shfl((int)v.x, pl, 64);
+        const uint32_t tv = in ? T[h] : 0u;
+        const uint32_t exact = lower ? xp : tv;
+        if (in && v.y != kKcIns) {
+            if (exact == kKcNone) F[h] = li;
+            else if ((v.y & 0x7fffffffu) != exact) kc_recheck(A, B, s, t, e, li, v.y, exact);
+        }
+        const uint64_t above = lane == 63 ? 0ull : (m >> (lane + 1));
+        if (in && above == 0) T[h] = v.x;
+    }
+    __syncthreads();
+    uint32_t *ft = B.ft + (s * (uint64_t)B.kmax + t) * 2 * (uint64_t)hs;
+    for (int32_t u = lane; u < hs; u += 64) {
+        ft[u] = F[u];
+        ft[hs + u] = T[u];
+    }
+}
+
+// a thread per (stream, hash): each segment's first read of the hash against the entry the
+// segments before it leave (0 at the stream start, K1x's table after its rounds); that entry is also
+// the next pass's table at the segment's start
+__global__ __launch_bounds__(256) void kc_v2(CompressArgs A, KcBufs B, int pass) {
+    const uint64_t gi = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t s = gi / (uint64_t)A.hs;
+    const uint32_t h = (uint32_t)(gi % (uint64_t)A.hs);
+    if (s >= A.count || (A.spec_mode != 0 && A.spec[s].flags != 0)) return;
+    if (!kc_checking(B, s, pass)) return;
+    const uint32_t ns = B.sinfo[kKcInfo * s];
+    uint32_t run = A.spec_mode != 0 ? A.spec_tab[s * (uint64_t)A.hs + h] : 0u;
+    for (uint32_t t = 0; t < ns; t++) {
+        const uint32_t *ft = B.ft + (s * (uint64_t)B.kmax + t) * 2 * (uint64_t)A.hs;
+        const uint32_t f = ft[h], w = ft[A.hs + h];
+        const uint32_t *e = B.seg + (s * (uint64_t)B.kmax + t) * kKcSegWords;
+        if (t > 0) {
+            const uint64_t c = s * (uint64_t)B.kmax + e[0];
+            B.t0[c * (uint64_t)A.hs + h] = run;
+            if (h == 0) B.cstart[c] = (int32_t)e[1];
+        }
+        if (f != kKcNone) {
+            const uint32_t got = B.log[(s * (uint64_t)B.kmax + e[0]) * (uint64_t)B.logcap + f].y;
+            if ((got & 0x7fffffffu) != run) kc_recheck(A, B, s, t, e, f, got, run);
+        }
+        if (w != kKcNone) run = w;
+    }
 }
 
 // K1L on a Writer handle (Writer.Write writer.go:206-337 on a stream at position start): one 16-lane
@@ -1888,6 +2309,226 @@ __global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t
     emit_stream<WIDE>(A, recs, rcap, s, lane, WIDE ? nullptr : &stage[WIDE ? 0 : w][0]);
 }
 
+// The token writer for 16-byte records (K1L, K1c) across the chip: k1_emit<true> walks a stream's
+// records with one wave, 64 at a time (C4s: 64 waves over ~180 k records each, 6.6 ms).  Here blocks
+// of kEwRec records each sum their tokens' sizes (ke_size), one wave per stream scans the block sums
+// after the header (ke_scan, which also decides the stream's size and status as emit_stream does),
+// and every block writes its tokens at their offsets (ke_write).  Tokens, literal bytes and the
+// trailing literal are emit_stream's; a token is written when it ends within the slot, and a slot
+// too small ends the output at the first token that does not fit (ENOSPC), as emit_stream's does.
+constexpr int32_t kEwRec = 2048, kEwPer = kEwRec / 256;
+struct EwBufs {
+    uint64_t *bsum;   // per (stream, block): the block's token bytes, then (ke_scan) its offset
+    uint64_t *info;   // per stream: {records, tail literal start, out end of the records, flags}
+    uint32_t nb;      // blocks per stream
+};
+// the size of record r's tokens (literal tag + bytes, copy tag + offset) and its literal (start, length)
+__device__ __forceinline__ int32_t ew_token(const uint4 *rec, int32_t r, int32_t done0, int32_t &lit_at, int32_t &L) {
+    const uint4 v = rec[r];
+    const int32_t dk = r == 0 ? done0 : (int32_t)(rec[r - 1].x + rec[r - 1].y);
+    L = (int32_t)v.x - dk;
+    lit_at = dk;
+    const bool lit = (v.w & 1) != 0 || L > 0;
+    int32_t ln = 0, tn = 0, on = 0;
+    (void)tag_bytes(0x00, L, &ln);
+    (void)tag_bytes(0x80, (int32_t)v.y, &tn);
+    (void)off_bytes((int32_t)v.z, (int32_t)v.y, &on);
+    if (v.y == 0) tn = on = 0;
+    return (lit ? ln + L : 0) + tn + on;
+}
+__device__ __forceinline__ void ew_stream(const CompressArgs &A, uint64_t s, int32_t &H, int32_t &done0, bool &skip) {
+    const bool spec = A.spec_mode != 0;
+    skip = spec && A.spec[s].flags != 0;
+    H = spec ? (int32_t)A.spec[s].op : (A.header ? (A.append_magic ? 9 : 3) : 0);
+    done0 = spec ? (int32_t)A.spec[s].done : 0;
+}
+
+__global__ __launch_bounds__(256) void ke_size(CompressArgs A, const uint4 *recs, uint64_t rcap, EwBufs E) {
+    __shared__ uint64_t part[4];
+    const uint64_t s = blockIdx.x / E.nb;
+    const uint32_t b = blockIdx.x % E.nb;
+    int32_t H, done0;
+    bool skip;
+    ew_stream(A, s, H, done0, skip);
+    const int32_t m = (int32_t)((A.out_size[s] & 0xffffffffffffull) < rcap ? (A.out_size[s] & 0xffffffffffffull) : rcap);
+    if (skip || (int64_t)b * kEwRec >= m) return;
+    const uint4 *rec = recs + s * rcap;
+    uint64_t sum = 0;
+    for (int32_t t = 0; t < kEwPer; t++) {
+        const int32_t r = (int32_t)b * kEwRec + t * 256 + (int32_t)threadIdx.x;
+        int32_t la, L;
+        if (r < m) sum += (uint64_t)ew_token(rec, r, done0, la, L);
+    }
+    for (int d = 32; d >= 1; d >>= 1) sum += (uint64_t)__shfl_xor((long long)sum, d, 64);
+    if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) E.bsum[s * E.nb + b] = part[0] + part[1] + part[2] + part[3];
+}
+
+// a wave per stream: block offsets, the header, the stream's size and status (emit_stream's rules)
+__global__ __launch_bounds__(64) void ke_scan(CompressArgs A, const uint4 *recs, uint64_t rcap, EwBufs E) {
+    const uint64_t s = blockIdx.x;
+    const int lane = (int)threadIdx.x;
+    int32_t H, done0;
+    bool skip;
+    ew_stream(A, s, H, done0, skip);
+    if (skip) return;
+    const int32_t n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+    uint8_t *out = A.out + A.out_off[s];
+    const int64_t cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
+    const uint64_t pr = A.out_size[s];
+    const int32_t m = (int32_t)((pr & 0xffffffffffffull) < rcap ? (pr & 0xffffffffffffull) : rcap);
+    int err = (int)(pr >> 48);
+    const bool spec = A.spec_mode != 0;
+    uint64_t *inf = E.info + 4 * s;
+    if (!spec && H > cap) {  // not even the header
+        if (lane == 0) {
+            inf[0] = 0, inf[3] = 1;
+            A.out_size[s] = 0;
+            if (A.status) A.status[s] = EZ_ENOSPC;
+        }
+        return;
+    }
+    if (lane == 0 && !spec && H > 0) {
+        const int32_t bsl = (int32_t)__builtin_ctzll((uint64_t)A.bs);
+        const uint64_t hm = A.append_magic ? (0x141080797a616502ull << 8 | 0x80) : (0x80ull | 0x10ull << 8 | (uint64_t)bsl << 16);
+        put_small(out, V16{hm, A.append_magic ? (uint64_t)bsl : 0ull}, (uint32_t)H);
+    }
+    const uint32_t nb = (uint32_t)((m + kEwRec - 1) / kEwRec);
+    uint64_t run = (uint64_t)H;
+    for (uint32_t b0 = 0; b0 < nb; b0 += 64) {
+        const uint32_t b = b0 + (uint32_t)lane;
+        const uint64_t v = b < nb ? E.bsum[s * E.nb + b] : 0;
+        uint64_t incl = v;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t u = (uint64_t)__shfl_up((long long)incl, d, 64);
+            if (lane >= d) incl += u;
+        }
+        if (b < nb) E.bsum[s * E.nb + b] = run + incl - v;
+        run += (uint64_t)__shfl((long long)incl, 63, 64);
+    }
+    if (lane != 0) return;
+    const int32_t tail_at = m > 0 ? (int32_t)(recs[s * rcap + m - 1].x + recs[s * rcap + m - 1].y) : done0;
+    inf[0] = (uint64_t)m, inf[1] = (uint64_t)tail_at, inf[2] = run, inf[3] = 0;
+    if ((int64_t)run > cap) {  // ke_write's block at the crossing sets the size
+        if (A.status) A.status[s] = err ? err : EZ_ENOSPC;
+        inf[3] = 2;
+        return;
+    }
+    uint64_t op = run;
+    if (!err && tail_at < n) {  // the trailing literal (writer.go:324-329): its tag here, its bytes in ke_write
+        const int32_t L = n - tail_at;
+        int32_t ln = 0;
+        const uint64_t lb = tag_bytes(0x00, L, &ln);
+        if ((int64_t)op + ln + L > cap) {
+            err = EZ_ENOSPC;
+        } else {
+            put_small(out + op, V16{lb, 0}, (uint32_t)ln);
+            inf[3] = 4 | ((uint64_t)(op + ln) << 8);  // (the tail's bytes go to op + ln)
+            op += ln + L;
+        }
+    }
+    A.out_size[s] = op;
+    if (A.status) A.status[s] = err;
+}
+
+__global__ __launch_bounds__(256) void ke_write(CompressArgs A, const uint4 *recs, uint64_t rcap, EwBufs E) {
+    __shared__ uint64_t wsum[4];
+    const uint64_t s = blockIdx.x / E.nb;
+    const uint32_t b = blockIdx.x % E.nb;
+    int32_t H, done0;
+    bool skip;
+    ew_stream(A, s, H, done0, skip);
+    if (skip) return;
+    const uint64_t *inf = E.info + 4 * s;
+    if (inf[3] == 1) return;
+    const int32_t m = (int32_t)inf[0];
+    const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
+    const uint8_t *p = A.in + A.in_off[s];
+    uint8_t *out = A.out + A.out_off[s];
+    const uint64_t cap = A.out_off[s + 1] - A.out_off[s];
+    const int lane = (int)(threadIdx.x & 63), w = (int)(threadIdx.x >> 6);
+    if ((int64_t)b * kEwRec < m) {
+        const uint4 *rec = recs + s * rcap;
+        // this thread's kEwPer consecutive records: sizes, then offsets by a block scan
+        const int32_t r0 = (int32_t)b * kEwRec + (int32_t)threadIdx.x * kEwPer;
+        uint64_t mine = 0;
+        for (int32_t t = 0; t < kEwPer; t++) {
+            int32_t la, L;
+            if (r0 + t < m) mine += (uint64_t)ew_token(rec, r0 + t, done0, la, L);
+        }
+        uint64_t incl = mine;
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint64_t u = (uint64_t)__shfl_up((long long)incl, d, 64);
+            if (lane >= d) incl += u;
+        }
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        uint64_t at = E.bsum[s * E.nb + b] + incl - mine;
+        for (int v = 0; v < w; v++) at += wsum[v];
+        for (int32_t t = 0; t < kEwPer; t++) {
+            const int32_t r = r0 + t;
+            const bool here = r < m;
+            int32_t dk = 0, L = 0, T = 0;
+            uint64_t lpos = 0;  // a long literal's output position
+            bool longlit = false;
+            if (here) {
+                T = ew_token(rec, r, done0, dk, L);
+                const uint4 v = rec[r];
+                if (at + (uint64_t)T <= cap) {
+                    uint8_t *d = out + at;
+                    const bool lit = (v.w & 1) != 0 || L > 0;
+                    int32_t ln = 0, tn = 0, on = 0;
+                    const uint64_t lb = tag_bytes(0x00, L, &ln);
+                    uint64_t tb = tag_bytes(0x80, (int32_t)v.y, &tn);
+                    uint64_t ob = off_bytes((int32_t)v.z, (int32_t)v.y, &on);
+                    if (v.y == 0) tb = ob = 0, tn = on = 0;
+                    if (lit) {
+                        put_small(d, V16{lb, 0}, (uint32_t)ln);
+                        if (L >= kLongLit) {
+                            longlit = true;
+                            lpos = at + (uint64_t)ln;
+                        } else {
+                            copy_lane(d + ln, p + dk, L, lo, hi);
+                        }
+                    }
+                    if (tn) {
+                        const uint64_t c0 = tb | (ob << (8 * tn));
+                        const uint64_t c1 = ob >> (64 - 8 * tn);
+                        put_small(d + T - tn - on, V16{c0, c1}, (uint32_t)(tn + on));
+                    }
+                } else if (at <= cap) {  // the first token that does not fit: the output ends before it
+                    A.out_size[s] = at;
+                }
+            }
+            // long literals: the whole wave, one at a time (as emit_stream)
+            for (uint64_t lm = __ballot(longlit); lm; lm &= lm - 1) {
+                const int src = __builtin_ctzll(lm);
+                const int32_t Ls = __shfl(L, src, 64), ds = __shfl(dk, src, 64);
+                const uint64_t ts = (uint64_t)__shfl((long long)lpos, src, 64);
+                for (int32_t q = 16 * lane; q < Ls; q += 16 * 64) {
+                    const V16 v = ld16_in(p + ds + q, lo, hi);
+                    if (q + 16 <= Ls) st16v(out + ts + q, v);
+                    else put_small(out + ts + q, v, (uint32_t)(Ls - q));
+                }
+            }
+            if (here) at += (uint64_t)T;
+        }
+    }
+    // the trailing literal's bytes, by the stream's blocks in turn
+    if (inf[3] & 4) {
+        const int32_t n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+        const int32_t ta = (int32_t)inf[1];
+        const int32_t L = n - ta;
+        const uint64_t ts = inf[3] >> 8;
+        for (int64_t q = ((int64_t)b * 256 + threadIdx.x) * 16; q < L; q += (int64_t)E.nb * 256 * 16) {
+            const V16 v = ld16_in(p + ta + q, lo, hi);
+            if (q + 16 <= L) st16v(out + ts + q, v);
+            else put_small(out + ts + q, v, (uint32_t)(L - q));
+        }
+    }
+}
+
 // LDS words of a stream's table (0 = this variant cannot take the batch)
 template <bool T16>
 uint32_t split_table_words(const CompressArgs &a) {
@@ -2010,8 +2651,10 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     // the window's region in LDS (WinLds; C1 K1 2.18 -> 2.08 ms, A/B on one box); EZ_K1S_LW=0 (A/B) keeps it in the lanes' registers
     static const bool lw = knob("EZ_K1S_LW", 1) != 0;
     // the judgement's forward cap: 40 bytes (48-byte windows and candidates; C1 K1 2.081 -> 2.012 ms,
-    // A/B on one box) or 24; EZ_K1S_FW=24 (A/B)
-    static const bool w40 = knob("EZ_K1S_FW", 40) == 40;
+    // A/B on one box) for streams up to 8 KiB, else 24 (the 16 and 64 KiB sweep points ran 9-12 %
+    // slower with 40); EZ_K1S_FW=40 or 24 (A/B) forces one
+    static const int fw = knob("EZ_K1S_FW", 0);
+    const bool w40 = fw == 40 || (fw == 0 && a.max_len <= 8192);
     // persistent groups (a stream queue); EZ_K1S_PERSIST=0 (A/B): one launch block per 4 streams
     static const bool persist = knob("EZ_K1S_PERSIST", 0) != 0;
     const size_t lds = (size_t)stride * 4 * S + (lw && msk ? (size_t)kWinLdsBytes * S : 0) + pad;
@@ -2168,9 +2811,187 @@ bool long_applies(const CompressArgs &a) {
     return !off && !a.ring && !a.write_idx && a.start == 0 && a.header && a.hs <= 4096 && a.hs >= 4 && a.max_len > 0 &&
            a.max_len < (1ull << 31) && lds_store32_in_lane_order();
 }
-uint64_t long_scratch_bytes(const CompressArgs &a) { return a.count * rec_cap(a) * sizeof(WideRec); }
+// K1c geometry: chunks of C positions, parses from W positions before a chunk to O past the next one's
+// start (EZ_K1C_C / _W / _O, experiment builds); event words and records per chunk
+struct KcGeom {
+    int32_t C, W, O, kmax, logcap;
+    uint32_t rcap_c;
+};
+static KcGeom kc_geom(const CompressArgs &a) {
+    static const int32_t C = knob("EZ_K1C_C", 32768), W = knob("EZ_K1C_W", 1024), O = knob("EZ_K1C_O", 1024);
+    KcGeom g;
+    g.C = C, g.W = W, g.O = O;
+    g.kmax = (int32_t)((a.max_len + (uint64_t)C - 1) / (uint64_t)C);
+    g.logcap = W + C + O + 2048;  // (re-visits: an accept short of x + 2 parses positions again)
+    g.rcap_c = (uint32_t)((C + O + 64) / 6 + 4);
+    return g;
+}
+static uint64_t up256(uint64_t x) { return (x + 255) & ~255ull; }
+struct KcLay {
+    uint64_t crec, log, meta, seg, sinfo, ft, cstart, t0, cfail, left, total;
+};
+static KcLay kc_layout(const CompressArgs &a, const KcGeom &g) {
+    const uint64_t nc = a.count * (uint64_t)g.kmax;
+    KcLay l;
+    uint64_t o = 0;
+    l.crec = o, o += up256(nc * g.rcap_c * sizeof(uint4));
+    l.log = o, o += up256(nc * (uint64_t)g.logcap * sizeof(uint2));
+    l.meta = o, o += up256(nc * sizeof(uint4));
+    l.seg = o, o += up256(nc * kKcSegWords * 4);
+    l.sinfo = o, o += up256(a.count * kKcInfo * 4);
+    l.ft = o, o += up256(nc * 2 * (uint64_t)a.hs * 4);
+    l.cstart = o, o += up256(nc * 4);
+    l.t0 = o, o += up256(nc * (uint64_t)a.hs * 4);
+    l.cfail = o, o += up256(nc * 4);
+    l.left = o, o += 256;
+    l.total = o;
+    return l;
+}
+
+// the chip-wide token writer's workspace (after K1L's records) and its launch: batches of at most
+// 1,024 streams (C4s 36.9 -> 30.9 ms; C2's 4,096 streams keep k1_emit<true>, one wave per stream:
+// 25.0 against 28.0 ms); EZ_K1E_WIDE=0 / 1 (experiment builds) forces either
+static uint32_t ew_blocks(const CompressArgs &a) { return (uint32_t)((rec_cap(a) + kEwRec - 1) / kEwRec); }
+static uint64_t ew_bytes(const CompressArgs &a) { return up256(a.count * ew_blocks(a) * 8) + up256(a.count * 32); }
+static hipError_t launch_emit_wide(const CompressArgs &a, const uint4 *recs, uint64_t rcap, uint8_t *ws, hipStream_t st) {
+    static const int wk = knob("EZ_K1E_WIDE", -1);
+    const bool wide = wk < 0 ? a.count <= 1024 : wk != 0;
+    if (!wide) {
+        hipLaunchKernelGGL(k1_emit<true>, dim3((unsigned)((a.count + 3) / 4)), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
+        return hipGetLastError();
+    }
+    EwBufs E;
+    E.nb = ew_blocks(a);
+    E.bsum = (uint64_t *)ws;
+    E.info = (uint64_t *)(ws + up256(a.count * E.nb * 8));
+    const unsigned g = (unsigned)(a.count * E.nb);
+    hipLaunchKernelGGL(ke_size, dim3(g), dim3(256), 0, st, a, recs, rcap, E);
+    hipLaunchKernelGGL(ke_scan, dim3((unsigned)a.count), dim3(64), 0, st, a, recs, rcap, E);
+    hipLaunchKernelGGL(ke_write, dim3(g), dim3(256), 0, st, a, recs, rcap, E);
+    return hipGetLastError();
+}
+
+// K1c takes K1L's batches of at most 1,024 streams at least two chunks long: there K1L runs at most
+// one wave per SIMD, each a latency chain over a whole stream (C4s, 64 x 4 MiB: K1 245 -> 31 ms;
+// 1,024 x 1 MiB: 115 -> 103 ms); C2's 4,096 streams keep K1L (25 ms against 64 for K1c's passes,
+// which are bound by the parse's instructions there).  EZ_K1C=0 / EZ_K1C_MAXCOUNT (experiment
+// builds) or a forced 'l': K1L alone
+bool chunk_applies(const CompressArgs &a) {
+    static const bool on = knob("EZ_K1C", 1) != 0;
+    static const uint64_t most = (uint64_t)knob("EZ_K1C_MAXCOUNT", 1024);
+    return on && !compress_forced_long() && long_applies(a) && a.count <= most && a.max_len >= 2 * (uint64_t)kc_geom(a).C;
+}
+
+// verdict counts of K1c batches while counting is on (ez_compress_k1c_stats)
+static bool g_kc_stats_on = false;
+static uint64_t g_kc_stats[6] = {0, 0, 0, 0, 0, 0};
+void k1c_stats(int enable, uint64_t *out) {
+    if (out)
+        for (int t = 0; t < 6; t++) out[t] = g_kc_stats[t];
+    if (enable)
+        for (int t = 0; t < 6; t++) g_kc_stats[t] = 0;
+    g_kc_stats_on = enable != 0;
+}
+
+static hipError_t launch_chunk(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
+    const KcGeom g = kc_geom(a);
+    const KcLay l = kc_layout(a, g);
+    const uint64_t rcap = rec_cap(a);
+    uint8_t *ews = recs + up256(a.count * rcap * sizeof(WideRec));
+    uint8_t *base = ews + ew_bytes(a);
+    KcBufs B;
+    B.crec = (uint4 *)(base + l.crec);
+    B.log = (uint2 *)(base + l.log);
+    B.meta = (uint4 *)(base + l.meta);
+    B.seg = (uint32_t *)(base + l.seg);
+    B.sinfo = (uint32_t *)(base + l.sinfo);
+    B.ft = (uint32_t *)(base + l.ft);
+    B.cstart = (int32_t *)(base + l.cstart);
+    B.t0 = (uint32_t *)(base + l.t0);
+    B.cfail = (uint32_t *)(base + l.cfail);
+    B.C = g.C, B.W = g.W, B.O = g.O, B.kmax = g.kmax, B.logcap = g.logcap, B.rcap_c = g.rcap_c;
+    const uint64_t nc = a.count * (uint64_t)g.kmax;
+    hipError_t e = hipSuccess;
+    static const bool lw = knob("EZ_K1L_LW", 1) != 0;
+    static bool attr_done = false;
+    if (!attr_done) {
+        (void)hipFuncSetAttribute((const void *)kc_parse<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)kc_parse<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_long<false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_long<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        attr_done = true;
+    }
+    const size_t lds = (size_t)4 * (size_t)a.hs * 4 + (lw ? (size_t)4 * kWinLdsBytes : 0);
+    const unsigned pgrid = (unsigned)((nc + 3) / 4);
+    // passes (EZ_K1C_PASSES, experiment builds; 1 = the speculative chunks alone): from the third on,
+    // the host reads how many streams are still failed and stops at none (C2 / C4s: all proven after
+    // 4 passes of 32 KiB chunks)
+    static const int passes = knob("EZ_K1C_PASSES", 12);
+    uint32_t *left = (uint32_t *)(base + l.left);
+    static const bool diag = knob("EZ_K1C_DIAG", 0) != 0;
+    for (int pass = 1; pass <= passes; pass++) {
+        if (lw) hipLaunchKernelGGL(kc_parse<true>, dim3(pgrid), dim3(64), lds, st, a, B, pass);
+        else hipLaunchKernelGGL(kc_parse<false>, dim3(pgrid), dim3(64), lds, st, a, B, pass);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        hipLaunchKernelGGL(kc_stitch, dim3((unsigned)((a.count + 63) / 64)), dim3(64), 0, st, a, B, rcap, pass);
+        hipLaunchKernelGGL(kc_gather, dim3((unsigned)nc), dim3(256), 0, st, a, B, (uint4 *)recs, rcap, pass);
+        hipLaunchKernelGGL(kc_v1, dim3((unsigned)nc), dim3(64), (size_t)2 * (size_t)a.hs * 4, st, a, B, pass);
+        hipLaunchKernelGGL(kc_v2, dim3((unsigned)((a.count * (uint64_t)a.hs + 255) / 256)), dim3(256), 0, st, a, B, pass);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        bool stop = false;
+        if (pass >= 3 && pass < passes) {
+            uint32_t h_left = 0;
+            if ((e = hipMemsetAsync(left, 0, 4, st)) != hipSuccess) return e;
+            hipLaunchKernelGGL(kc_count, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, st, a, B, left);
+            if ((e = hipMemcpyAsync(&h_left, left, 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+            if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+            stop = h_left == 0;
+        }
+        const bool final = stop || pass == passes;
+        if (!(diag || (g_kc_stats_on && final))) {
+            if (stop) break;
+            continue;
+        }
+        // (tests, experiment builds) the verdicts: wait for them and count
+        std::vector<uint32_t> si(a.count * kKcInfo);
+        std::vector<SpecState> sp(a.spec_mode != 0 ? a.count : 0);
+        if ((e = hipMemcpyAsync(si.data(), B.sinfo, si.size() * 4, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+        if (!sp.empty() && (e = hipMemcpyAsync(sp.data(), a.spec, sp.size() * sizeof(SpecState), hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        uint64_t f[16] = {0}, segs = 0;
+        for (uint64_t s = 0; s < a.count; s++) {
+            if (!sp.empty() && sp[s].flags != 0) continue;  // (finished by K1x)
+            f[si[kKcInfo * s + 1] & 15]++;
+            segs += si[kKcInfo * s];
+        }
+        const uint64_t v[6] = {f[0], f[kKcFailChunk], f[kKcFailSync], f[kKcFailJudge], f[kKcFailCap], segs};
+        if (g_kc_stats_on && final)
+            for (int t = 0; t < 6; t++) g_kc_stats[t] += v[t];
+        if (diag)
+            fprintf(stderr, "K1c pass %d: %llu streams x %d chunks; proven %llu, chunk %llu, sync %llu, judge %llu, cap %llu; segments %llu\n",
+                    pass, (unsigned long long)a.count, g.kmax, (unsigned long long)v[0], (unsigned long long)v[1], (unsigned long long)v[2],
+                    (unsigned long long)v[3], (unsigned long long)v[4], (unsigned long long)v[5]);
+        if (stop) break;
+    }
+    // the fallback: K1L from the start (or K1x's state) for the streams K1c could not prove
+    const uint32_t S = a.count <= 256 ? 1u : 4u;
+    const size_t llds = (size_t)S * (size_t)a.hs * 4 + (lw ? (size_t)4 * kWinLdsBytes : 0);
+    const unsigned lgrid = (unsigned)((a.count + S - 1) / S);
+    if (lw) hipLaunchKernelGGL(k1_long<true>, dim3(lgrid), dim3(64), llds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S, B.sinfo + 1, kKcInfo);
+    else hipLaunchKernelGGL(k1_long<false>, dim3(lgrid), dim3(64), llds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S, B.sinfo + 1, kKcInfo);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    return launch_emit_wide(a, (const uint4 *)recs, rcap, ews, st);
+}
+
+// [K1L's records][the token writer's workspace][K1c's workspace]
+uint64_t long_scratch_bytes(const CompressArgs &a) {
+    const uint64_t r = up256(a.count * rec_cap(a) * sizeof(WideRec)) + ew_bytes(a);
+    return chunk_applies(a) ? r + kc_layout(a, kc_geom(a)).total : r;
+}
 
 hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
+    if (chunk_applies(a)) return launch_chunk(a, recs, st);
     // streams per wave: one for batches of a few hundred streams (C4s' 64: K1 361 -> 291 ms), else 4
     // (each wave's instructions serve 4 streams; C2's 4,096 streams: 32.3 ms at 4, 33.5 at 2, 38.2 at
     // 1; 1,024 x 1 MiB compressed at 7.3 GiB/s at 1 against 7.6 at 4); EZ_K1L_SPW=1|2|4 overrides
@@ -2187,12 +3008,11 @@ hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
         attr_done = true;
     }
     const unsigned grid = (unsigned)((a.count + S - 1) / S);
-    if (lw) hipLaunchKernelGGL(k1_long<true>, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S);
-    else hipLaunchKernelGGL(k1_long<false>, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S);
+    if (lw) hipLaunchKernelGGL(k1_long<true>, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S, nullptr, 0u);
+    else hipLaunchKernelGGL(k1_long<false>, dim3(grid), dim3(64), lds, st, a, (uint32_t)a.hs, (uint4 *)recs, rcap, S, nullptr, 0u);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k1_emit<true>, dim3((unsigned)((a.count + 3) / 4)), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
-    return hipGetLastError();
+    return launch_emit_wide(a, (const uint4 *)recs, rcap, recs + up256(a.count * rcap * sizeof(WideRec)), st);
 }
 
 // K1L for one Write on a Writer handle (writer_run): single Writes of 16 bytes .. 64 MiB on

@@ -147,6 +147,10 @@ bool long_ring_applies(const CompressArgs &a);
 uint64_t long_ring_scratch_bytes(const CompressArgs &a);
 hipError_t launch_long_ring(const CompressArgs &a, uint8_t *recs, hipStream_t s);
 bool compress_forced_general();  // ez_select_compress_kernel('w') (tests, A/B)
+bool compress_forced_long();     // ez_select_compress_kernel('l'): K1L alone, without K1c (tests, A/B)
+// K1c (chunk-parallel K1L, ez_compress_split.hip): counting of its verdicts (ez_compress_k1c_stats)
+bool chunk_applies(const CompressArgs &a);
+void k1c_stats(int enable, uint64_t *out);
 // K1x: the data-parallel first pass for long fresh single-Write streams (ez_compress_spec.hip)
 bool spec_applies(const CompressArgs &a, bool any_len = false);  // any_len: also below 64 KiB (forced)
 uint64_t spec_scratch_bytes(const CompressArgs &a);

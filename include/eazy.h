@@ -252,6 +252,12 @@ int ez_select_decompress_kernel(int kind);
 /* Introspection: the first K2 kernel the last ez_decompress_batch call of this process ran
  * ('r', 't', 'w'; 'e' the exact decoder alone; 0 none yet). */
 int ez_decompress_kernel_last(void);
+/* Testing: K1c (the chunk-parallel parse of long fresh streams, which proves each stream's parse
+ * is Go's or gives it to K1L) counts its verdicts while counting is on: counts (6 words, may be
+ * NULL) gets {streams proven, chunk error or re-visit, no common copy end, a judgement changed,
+ * record slot, path segments} so far; enable 1 clears them and turns counting on (each K1c batch
+ * then waits for its verdicts), 0 turns it off. */
+int ez_compress_k1c_stats(int enable, uint64_t *counts);
 
 #ifdef __cplusplus
 }
