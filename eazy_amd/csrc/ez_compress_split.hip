@@ -46,6 +46,7 @@
 #include "ez_k1_common.h"
 
 #include <cstdio>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -582,43 +583,40 @@ struct WinRoll {
 // of ten ds_bpermute, nine selects and eight v_alignbyte from the lanes' registers.  R: the
 // farthest window start the region serves (80 for 32-byte windows; 64 for the 48-byte windows of
 // the 40-byte judgement, whose bytes reach i + 15 + 39)
-template <int R = 80>
+template <int R = 80, int G = 16>
 struct WinLds {
-    uint32_t f0, f1;  // this lane's dwords of the prefetched region
+    static constexpr int LB = 128 / G;  // bytes of the 128-byte region per lane (8 or 16)
+    typedef unsigned int u32v __attribute__((ext_vector_type(LB / 4)));
+    u32v f;  // this lane's dwords of the prefetched region
     int32_t cb, fb, bmax, pm;
     uint8_t *wl;  // the group's buffer (LDS)
     __device__ __forceinline__ int32_t floor4(int32_t y) const { return y - ((pm + y) & 3); }
-    __device__ __forceinline__ void ld(const uint8_t *p, int32_t b, int lj, uint32_t &d0, uint32_t &d1) const {
-        typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
-        typedef const __attribute__((address_space(1))) u32x2 *gu64p;
-        const u32x2 v = *(gu64p)(p + b + 8 * lj);
-        d0 = v.x;
-        d1 = v.y;
+    __device__ __forceinline__ void ld(const uint8_t *p, int32_t b, int lj, u32v &d) const {
+        typedef const __attribute__((address_space(1))) u32v *gp;
+        d = *(gp)(p + b + LB * lj);
     }
-    __device__ __forceinline__ void put(int lj) const {
-        *(uint64_t *)(wl + 8 * lj) = (uint64_t)f0 | ((uint64_t)f1 << 32);
-    }
+    __device__ __forceinline__ void put(int lj) const { *(u32v *)(wl + LB * lj) = f; }
     __device__ __forceinline__ void init(const uint8_t *p, int32_t n, int lj, bool live) {
         pm = (int32_t)((uintptr_t)p & 3);
         bmax = floor4(n - 64);
         cb = min(floor4(-8), bmax);
         fb = min(cb + 64, bmax);
-        f0 = f1 = 0;
-        if (live) ld(p, cb, lj, f0, f1);
+        f = u32v{};
+        if (live) ld(p, cb, lj, f);
         put(lj);
-        if (live) ld(p, fb, lj, f0, f1);
+        if (live) ld(p, fb, lj, f);
     }
     __device__ __forceinline__ void advance(const uint8_t *p, int32_t i, int lj, bool live) {
         const int32_t y = i - 8;
         if (live && !(y >= cb && y - cb <= R)) {
             if (!(y >= fb && y - fb <= R)) {
                 fb = min(floor4(y), bmax);
-                ld(p, fb, lj, f0, f1);
+                ld(p, fb, lj, f);
             }
             cb = fb;
             put(lj);
             fb = min(cb + 64, bmax);
-            ld(p, fb, lj, f0, f1);
+            ld(p, fb, lj, f);
         }
     }
     __device__ __forceinline__ void bytes(int32_t i, int g, int lj, V16 &w0, V16 &w1) const {
@@ -809,6 +807,9 @@ __device__ __forceinline__ void lds_put12(uint64_t *tab, uint32_t h, uint32_t va
     asm volatile("ds_mskor_b64 %0, %1, %2" : : "v"(addr), "v"(m), "v"(v) : "memory");
 }
 
+#if (EZ_EXP & 65536)
+__device__ unsigned long long g_lean_hist[18];
+#endif
 constexpr int kEdgeSlots = 40;
 constexpr int32_t kEdgeBefore = 64;  // readable bytes before a stream (WinRoll's regions), 64 after it
 __host__ __device__ __forceinline__ uint64_t edge_slot_bytes(const CompressArgs &a) { return (a.max_len + kEdgeBefore + 64 + 15) & ~15ull; }
@@ -821,10 +822,11 @@ __host__ __device__ __forceinline__ uint64_t edge_area_bytes(const CompressArgs 
 // PERSIST: a group whose stream ends takes the next one from the batch's queue (a global counter)
 // instead of idling until the wave's other three groups end theirs; the grid is then the resident
 // waves of the chip, and a wave ends when the queue is empty and its groups are done.
-template <int TB, bool LW, int FW, bool PERSIST>
+template <int TB, bool LW, int FW, bool PERSIST, int G = 16>
 __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, uint16_t *hth, uint32_t table_words, uint32_t hsh,
                                          uint64_t *recs, uint64_t rcap, int prio, uint8_t *edge, uint8_t *wl) {
-    constexpr int G = 16, S = 64 / G;
+    constexpr int S = 64 / G;
+    constexpr uint32_t kGMask = (1u << G) - 1;
     constexpr bool W40 = FW == 40;
     static_assert(FW == 24 || (W40 && LW), "the 40-byte judgement reads its windows from the LDS region");
     constexpr int32_t CAP = W40 ? 40 : kFwdCap;
@@ -841,7 +843,8 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
     bool live = false, pending = false;
     uint64_t *rec = recs;
     V16 z0{0, 0}, z1{0, 0}, z2{0, 0};
-    typename std::conditional<LW, WinLds<W40 ? 64 : 80>, WinRoll>::type wr;
+    static_assert(G == 16 || LW, "8-lane groups read their windows from the LDS region");
+    typename std::conditional<LW, WinLds<W40 ? 64 : 80, G>, WinRoll>::type wr;
     if constexpr (LW) wr.wl = wl;
     // iterations left to the wave (SALU): every stream opened adds its parse's bound, so a correct
     // parse never reaches 0 and a wrong one cannot hang the grid
@@ -990,8 +993,11 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
                   (jb == 8 && bl > 8 ? 2 : 0);
         }
         const uint64_t am64 = __ballot(acc);
-        const uint32_t am = (uint32_t)(am64 >> (G * g)) & 0xffffu;
+        const uint32_t am = (uint32_t)(am64 >> (G * g)) & kGMask;
         const int a = am ? __builtin_ctz(am) : -1;
+#if (EZ_EXP & 65536)
+        if (live && lj == 0) atomicAdd(&g_lean_hist[a + 1], 1ull);  // (experiment builds: the acceptor lane, -1 none)
+#endif
         const bool act = live && a >= 0;
         // the group's next position, whether the acceptor needs an exact extension, and whether it
         // makes the i+1 insert (a window match, writer.go:315-318)
@@ -2117,19 +2123,19 @@ template <bool WIDE>
 __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
                                             uint64_t *stage = nullptr);
 
-template <int TB, bool LW = false, int FW = 24, bool PERSIST = false>
+template <int TB, bool LW = false, int FW = 24, bool PERSIST = false, int G = 16>
 __global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                  uint64_t rcap, int prio, uint8_t *edge) {
-    constexpr int G = 16, S = 64 / G;
+    constexpr int S = 64 / G;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = (int)(threadIdx.x & 63);
     const int g = lane / G, lj = lane % G;
     const int32_t hs = (int32_t)A.hs;
     const uint32_t hsh = 32u - (uint32_t)(64 - __builtin_clzll((uint64_t)(hs - 1)));
     uint16_t *hth = (uint16_t *)((uint32_t *)smem + (uint32_t)g * stride_words);
-    // (LW: the groups' window buffers after the four tables)
+    // (LW: the groups' window buffers after the S tables)
     uint8_t *wl = smem + (size_t)4 * stride_words * S + (size_t)g * kWinLdsBytes;
-    lean_run<TB, LW, FW, PERSIST>(A, lj, g, hth, table_words, hsh, recs, rcap, prio, edge, wl);
+    lean_run<TB, LW, FW, PERSIST, G>(A, lj, g, hth, table_words, hsh, recs, rcap, prio, edge, wl);
 }
 
 // ---------------------------------------------------------------- K1e
@@ -2591,14 +2597,14 @@ bool split_lean() {
     return v;
 }
 // resident blocks of a k1_lean variant on the device (per process; the persistent grid)
-template <int TB, bool LW, int FW, bool PERSIST>
+template <int TB, bool LW, int FW, bool PERSIST, int G>
 unsigned lean_resident(size_t lds) {
     static unsigned cached = 0;
     static size_t cached_lds = 0;
     if (cached == 0 || cached_lds != lds) {
         int dev = 0, cus = 0, per = 0;
         if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k1_lean<TB, LW, FW, PERSIST>, 64, lds) != hipSuccess || per <= 0 ||
+            hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, (const void *)k1_lean<TB, LW, FW, PERSIST, G>, 64, lds) != hipSuccess || per <= 0 ||
             cus <= 0)
             return 0;
         cached = (unsigned)(per * cus);
@@ -2607,22 +2613,23 @@ unsigned lean_resident(size_t lds) {
     return cached;
 }
 
-template <int TB, bool LW, int FW>
+template <int TB, bool LW, int FW, int G = 16>
 hipError_t launch_lean_v(const CompressArgs &a, uint64_t *recs, uint32_t stride, uint32_t tw, size_t lds, int prio, uint8_t *edge,
                          bool persist, hipStream_t st) {
     static bool attr_done = false;
     if (!attr_done) {
-        (void)hipFuncSetAttribute((const void *)k1_lean<TB, LW, FW, false>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-        (void)hipFuncSetAttribute((const void *)k1_lean<TB, LW, FW, true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<TB, LW, FW, false, G>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        (void)hipFuncSetAttribute((const void *)k1_lean<TB, LW, FW, true, G>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
+    constexpr uint64_t S = 64 / G;
     const uint64_t rcap = rec_cap(a);
-    const uint64_t blocks = (a.count + 3) / 4;
-    const unsigned res = persist ? lean_resident<TB, LW, FW, true>(lds) : 0;
+    const uint64_t blocks = (a.count + S - 1) / S;
+    const unsigned res = persist ? lean_resident<TB, LW, FW, true, G>(lds) : 0;
     if (res != 0 && blocks > res)
-        hipLaunchKernelGGL((k1_lean<TB, LW, FW, true>), dim3(res), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
+        hipLaunchKernelGGL((k1_lean<TB, LW, FW, true, G>), dim3(res), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
     else
-        hipLaunchKernelGGL((k1_lean<TB, LW, FW, false>), dim3((unsigned)blocks), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
+        hipLaunchKernelGGL((k1_lean<TB, LW, FW, false, G>), dim3((unsigned)blocks), dim3(64), lds, st, a, stride, tw, recs, rcap, prio, edge);
     return hipGetLastError();
 }
 
@@ -2633,7 +2640,15 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     static const bool msk = knob("EZ_K1S_MSK", 1) != 0 && lds_mskor_in_lane_order();
     static const bool m12 = msk && knob("EZ_K1S_T12", 0) != 0 && lds_mskor64_in_lane_order();
     const bool t12 = m12 && a.max_len <= 4099 && a.hs <= 4096;
-    constexpr int S = 4;
+    // 8-lane groups (8 streams per wave) for streams over 4 KiB: a window's acceptor is one of lanes
+    // 0..7 in 74 % of C1's windows (6.3 of 16 lanes are visits on average), so half-width windows
+    // take ~37 % fewer wave iterations; with the same streams per CU (the tables bound them) but half
+    // the waves, C1 measured 2.01 -> 2.14 ms, 8 KiB streams 8.58 -> 8.11, 16 KiB 11.06 -> 9.49 (with
+    // the 40-byte judgement), 64 KiB 14.10 -> 11.67.  EZ_K1S_G=8 / 16 (A/B) forces one
+    static const int gw = knob("EZ_K1S_G", 0);
+    const bool g8 = (gw == 8 || (gw == 0 && a.max_len > 4096)) && !t12 && msk && knob("EZ_K1S_LW", 1) != 0 &&
+                    split_stride<8, true>(a) != 0;
+    const int S = g8 ? 8 : 4;
     const uint32_t w12 = (uint32_t)((2 * ((a.hs + 4) / 5) + 3) & ~3ll);  // u32 words of a 12-bit table
     const uint32_t stride = t12 ? w12 : split_stride<16, true>(a), tw = t12 ? w12 : split_table_words<true>(a);
     const uint64_t rcap = rec_cap(a);
@@ -2651,15 +2666,19 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     // the window's region in LDS (WinLds; C1 K1 2.18 -> 2.08 ms, A/B on one box); EZ_K1S_LW=0 (A/B) keeps it in the lanes' registers
     static const bool lw = knob("EZ_K1S_LW", 1) != 0;
     // the judgement's forward cap: 40 bytes (48-byte windows and candidates; C1 K1 2.081 -> 2.012 ms,
-    // A/B on one box) for streams up to 8 KiB, else 24 (the 16 and 64 KiB sweep points ran 9-12 %
-    // slower with 40); EZ_K1S_FW=40 or 24 (A/B) forces one
+    // A/B on one box) for streams up to 8 KiB (16 KiB with 8-lane groups: 9.79 -> 9.49 ms), else 24
+    // (16-lane groups at 16 and 64 KiB ran 9-12 % slower with 40; 8-lane at 64 KiB 11.67 against
+    // 11.77); EZ_K1S_FW=40 or 24 (A/B) forces one
     static const int fw = knob("EZ_K1S_FW", 0);
-    const bool w40 = fw == 40 || (fw == 0 && a.max_len <= 8192);
+    const bool w40 = fw == 40 || (fw == 0 && a.max_len <= (g8 ? 16384u : 8192u));
     // persistent groups (a stream queue); EZ_K1S_PERSIST=0 (A/B): one launch block per 4 streams
     static const bool persist = knob("EZ_K1S_PERSIST", 0) != 0;
     const size_t lds = (size_t)stride * 4 * S + (lw && msk ? (size_t)kWinLdsBytes * S : 0) + pad;
     hipError_t e;
-    if (lw && msk) {
+    if (g8) {
+        if (w40) e = launch_lean_v<16, true, 40, 8>(a, recs, stride, tw, lds, prio, edge, persist, st);
+        else e = launch_lean_v<16, true, 24, 8>(a, recs, stride, tw, lds, prio, edge, persist, st);
+    } else if (lw && msk) {
         if (t12) e = launch_lean_v<12, true, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
         else if (w40) e = launch_lean_v<16, true, 40>(a, recs, stride, tw, lds, prio, edge, persist, st);
         else e = launch_lean_v<16, true, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
@@ -2670,6 +2689,22 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     else
         e = launch_lean_v<0, false, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
     if (e != hipSuccess) return e;
+#if (EZ_EXP & 65536)
+    {  // (experiment builds) the acceptor-lane histogram of this launch
+        unsigned long long hst[18];
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpyFromSymbol(hst, HIP_SYMBOL(g_lean_hist), sizeof hst);
+        unsigned long long tot = 0, vis = 0;
+        for (int t = 0; t < 18; t++) tot += hst[t];
+        for (int t = 1; t < 17; t++) vis += hst[t] * (unsigned long long)t;
+        vis += hst[0] * 16ull;
+        fprintf(stderr, "lean windows %llu (no accept %llu); visited lanes %.3f of 16; by acceptor lane:", tot, hst[0], (double)vis / (double)tot);
+        for (int t = 1; t < 17; t++) fprintf(stderr, " %.3f", (double)hst[t] / (double)tot);
+        fprintf(stderr, "\n");
+        memset(hst, 0, sizeof hst);
+        (void)hipMemcpyToSymbol(HIP_SYMBOL(g_lean_hist), hst, sizeof hst);
+    }
+#endif
     const unsigned egrid = (unsigned)((a.count + 3) / 4);
     hipLaunchKernelGGL(k1_emit<false>, dim3(egrid), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);
     return hipGetLastError();
