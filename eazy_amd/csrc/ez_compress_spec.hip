@@ -47,6 +47,11 @@ constexpr int64_t kPiece = 256;       // kx_judge: positions per block step
 static_assert(kChunk % kPiece == 0, "kx_judge reads one kx_pred chunk's table per piece");
 constexpr int64_t kCopyPiece = 65536; // kx_copy: bytes per block step
 constexpr int kRounds = 8;            // rounds before the general kernel takes the rest (EZ_K1X_ROUNDS)
+// A stream whose accepted position lay within kDenseGap bytes of the round's start in kDenseRounds
+// rounds in a row is dense (logs, C4s: one accepted position per round, ~180 k per stream): it
+// leaves the rounds for the continuation (K1c / K1L); C4 fp32 has no accepted position and C4h a
+// handful per stream.  (Counted in kx_judge instead, any store there cost kx_judge 1 ms at C4.)
+constexpr uint32_t kDenseGap = 256, kDenseRounds = 2, kHanded = 0xffffffffu;
 
 struct KxBufs {
     uint64_t kmax;     // chunks per stream
@@ -56,6 +61,7 @@ struct KxBufs {
     uint32_t *act;     // active streams of the round
     uint32_t *nact;    // [0] active count, [1] literal records
     uint64_t lit_cap;  // literal records reserved
+    uint32_t *dense;   // per stream: {the round's start (kNone before round 1), dense rounds in a row (kHanded: left)}
 };
 
 __device__ __forceinline__ uint32_t hash4(const uint8_t *q, uint32_t hsh) {
@@ -80,6 +86,8 @@ __global__ __launch_bounds__(64) void kx_init(CompressArgs A, KxBufs B) {
     h.put(0x80); h.put(0x10); h.put((uint32_t)__builtin_ctzll((uint64_t)A.bs));
     const int64_t cap = (int64_t)(A.out_off[s + 1] - A.out_off[s]);
     B.first[s] = 0;  // active in round 1
+    B.dense[2 * s] = kNone;
+    B.dense[2 * s + 1] = 0;
     // the launcher sized the scratch from max_len: longer streams are refused (as K1s does);
     // a header that does not fit is not written (put_hdr)
     const int err = (uint64_t)slen(A, s) > A.max_len ? EZ_EINVAL : (h.n > cap ? EZ_ENOSPC : EZ_OK);
@@ -167,16 +175,25 @@ __device__ void kx_tail(const CompressArgs &A, const KxBufs &B, uint64_t s) {
 }
 
 // one block: finish the streams whose last round accepted nothing, list the active ones
-__global__ __launch_bounds__(1024) void kx_reset(CompressArgs A, KxBufs B) {
+__global__ __launch_bounds__(1024) void kx_reset(CompressArgs A, KxBufs B, uint32_t dense_rounds) {
     __shared__ uint32_t cnt;
     if (threadIdx.x == 0) cnt = 0;
     __syncthreads();
     for (uint64_t s = threadIdx.x; s < A.count; s += 1024) {
-        if (A.spec[s].flags != 0) continue;
-        if (B.first[s] == kNone) {
+        if (A.spec[s].flags != 0 || B.dense[2 * s + 1] == kHanded) continue;
+        const uint32_t f = B.first[s];
+        if (f == kNone) {
             kx_tail(A, B, s);
+            continue;
+        }
+        const uint32_t rs = B.dense[2 * s];
+        const uint32_t streak = rs != kNone && f - rs < kDenseGap ? B.dense[2 * s + 1] + 1 : 0u;
+        B.first[s] = kNone;
+        if (dense_rounds != 0 && streak >= dense_rounds) {  // dense: the continuation takes it
+            B.dense[2 * s + 1] = kHanded;
         } else {
-            B.first[s] = kNone;
+            B.dense[2 * s] = A.spec[s].from;
+            B.dense[2 * s + 1] = streak;
             B.act[atomicAdd(&cnt, 1u)] = (uint32_t)s;
         }
     }
@@ -365,7 +382,7 @@ int rounds() {
 }
 
 struct Layout {
-    uint64_t pred, tabs, first, spec, spec_tab, act, nact, lit, lrec, total, lit_cap;
+    uint64_t pred, tabs, first, spec, spec_tab, act, nact, dense, lit, lrec, total, lit_cap;
 };
 
 Layout layout(const CompressArgs &a) {
@@ -380,7 +397,8 @@ Layout layout(const CompressArgs &a) {
     l.spec_tab = l.spec + up(a.count * sizeof(SpecState));
     l.act = l.spec_tab + up(a.count * (uint64_t)a.hs * 4);
     l.nact = l.act + up(a.count * 4);
-    l.lit = l.nact + 256;
+    l.dense = l.nact + 256;
+    l.lit = l.dense + up(a.count * 8);
     l.lrec = l.lit + up(l.lit_cap * sizeof(SpecLit));
     l.total = l.lrec + (long_applies(a) ? up(long_scratch_bytes(a)) : 0);  // K1L's records
     return l;
@@ -412,6 +430,7 @@ hipError_t launch_compress_spec(const CompressArgs &a0, uint8_t *scratch, hipStr
     B.first = (uint32_t *)(scratch + l.first);
     B.act = (uint32_t *)(scratch + l.act);
     B.nact = (uint32_t *)(scratch + l.nact);
+    B.dense = (uint32_t *)(scratch + l.dense);
     B.lit_cap = l.lit_cap;
     CompressArgs a = a0;
     a.spec = (SpecState *)(scratch + l.spec);
@@ -431,8 +450,9 @@ hipError_t launch_compress_spec(const CompressArgs &a0, uint8_t *scratch, hipStr
     hipLaunchKernelGGL(kx_scan, dim3((unsigned)((a.count * (uint64_t)a.hs + 255) / 256)), dim3(256), 0, st, a, B);
     if (!check()) return e;
     const unsigned jgrid = 2048;  // 8 blocks of 4 waves per CU
+    static const uint32_t dense_rounds = (uint32_t)knob("EZ_K1X_DENSE", (int)kDenseRounds);  // (0: never, A/B)
     for (int r = 0; r < rounds(); r++) {
-        hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B);
+        hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B, dense_rounds);
         if (!check()) return e;
         hipLaunchKernelGGL(kx_judge, dim3(jgrid), dim3(256), 0, st, a, B);
         if (!check()) return e;
@@ -443,7 +463,7 @@ hipError_t launch_compress_spec(const CompressArgs &a0, uint8_t *scratch, hipStr
     }
     // the streams still active (dense accepts, C4s): K1L from where they stand (the general kernel
     // where K1L cannot take the batch); then every recorded literal's bytes
-    hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B);
+    hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B, dense_rounds);
     if (!check()) return e;
     a.spec_mode = 2;
     if (long_applies(a0)) e = launch_long(a, scratch + l.lrec, st);
