@@ -1839,30 +1839,17 @@ __device__ __forceinline__ uint32_t kc_lower(const uint4 *r, uint32_t lo, uint32
     return lo;
 }
 
-// a thread per stream
-__global__ __launch_bounds__(64) void kc_stitch(CompressArgs A, KcBufs B, uint64_t rcap, int pass) {
-    const uint64_t s = (uint64_t)blockIdx.x * 64 + threadIdx.x;
-    if (s >= A.count) return;
-    if (A.spec_mode != 0 && A.spec[s].flags != 0) return;
-    uint32_t *si = B.sinfo + kKcInfo * s;
-    if (pass > 1 && si[1] != kKcFailJudge) return;
+// the sequential stitch of stream s (one thread): chunk o's path up to the first copy end it shares
+// with a later chunk's parse (or that chunk's start), then that chunk's; returns the failure code
+__device__ uint32_t kc_stitch_seq(const CompressArgs &A, const KcBufs &B, uint64_t s, int32_t K, int32_t from0, int32_t n,
+                                  int32_t &nseg, uint32_t &tot) {
     const uint64_t c0 = s * (uint64_t)B.kmax;
-    const int32_t n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
-    const int32_t from0 = A.spec_mode != 0 ? (int32_t)A.spec[s].from : 0;
-    uint32_t fail = 0;
-    int32_t K = 0;
-    for (int32_t k = 0; k < B.kmax; k++) {
-        const uint4 m = B.meta[c0 + k];
-        if (!(m.y & kKcHave)) break;
-        if (m.y & (kKcErr | kKcBad)) fail = kKcFailChunk;
-        K++;
-        if (m.y & kKcLast) break;
-    }
-    uint32_t *seg = B.seg + s * (uint64_t)B.kmax * kKcSegWords;
-    int32_t nseg = 0;
-    uint32_t tot = 0, ri = 0, li = 0;
+    uint32_t *seg = B.seg + c0 * kKcSegWords;
+    uint32_t ri = 0, li = 0;
     int32_t o = 0, q = from0;
-    while (!fail && K > 0) {
+    nseg = 0;
+    tot = 0;
+    for (;;) {
         const uint4 mo = B.meta[c0 + o];
         const uint32_t no = mo.x;
         const uint4 *ro = B.crec + (c0 + o) * (uint64_t)B.rcap_c;
@@ -1871,13 +1858,12 @@ __global__ __launch_bounds__(64) void kc_stitch(CompressArgs A, KcBufs B, uint64
             e[0] = (uint32_t)o, e[1] = (uint32_t)q, e[2] = (uint32_t)n, e[3] = ri, e[4] = no, e[5] = tot, e[6] = li, e[7] = mo.z;
             nseg++;
             tot += no - ri;
-            break;
+            return 0;
         }
         const int32_t xl = no > ri ? kc_nx(ro[no - 1]) : -1;  // this parse's last copy end
-        bool found = false;
+        bool found = false, virt = false;
         uint32_t fa = 0, fb = 0;
         int32_t fj = 0, Q = 0;
-        bool virt = false;
         for (int32_t j = o + 1; j < K && !found && (int64_t)from0 + (int64_t)j * B.C <= xl; j++) {
             const int32_t bj = (int32_t)((int64_t)from0 + (int64_t)j * B.C);
             const uint4 mj = B.meta[c0 + j];
@@ -1903,10 +1889,7 @@ __global__ __launch_bounds__(64) void kc_stitch(CompressArgs A, KcBufs B, uint64
                 else ib++;
             }
         }
-        if (!found) {
-            fail = kKcFailSync;
-            break;
-        }
+        if (!found) return kKcFailSync;
         e[0] = (uint32_t)o, e[1] = (uint32_t)q, e[2] = (uint32_t)Q, e[3] = ri, e[4] = fa + 1, e[5] = tot, e[6] = li, e[7] = kc_li(ro[fa]);
         nseg++;
         tot += fa + 1 - ri;
@@ -1914,14 +1897,129 @@ __global__ __launch_bounds__(64) void kc_stitch(CompressArgs A, KcBufs B, uint64
         li = virt ? 0u : kc_li(rj[fb]);
         o = fj, q = Q, ri = virt ? 0u : fb + 1;
     }
+}
+
+// a wave per stream.  Every boundary k -> k+1 at once: the first copy end at or after b_k+1 that
+// chunk k's parse shares with chunk k+1's (or chunk k+1's start); when every boundary has one and
+// they increase, the segments are the chunks themselves and their record offsets a scan; else (a
+// copy across a whole chunk, no shared end) the sequential stitch decides (C4s: 0.62 ms a pass
+// for 64 streams x 128 chunks with the sequential one alone)
+constexpr int32_t kKcPar = 1024;  // chunks the parallel stitch takes
+constexpr uint32_t kKcVirt = 0xfffffffdu, kKcNoJoin = 0xfffffffcu;
+__global__ __launch_bounds__(64) void kc_stitch(CompressArgs A, KcBufs B, uint64_t rcap, int pass) {
+    __shared__ int32_t sQ[kKcPar];
+    __shared__ uint32_t sfa[kKcPar], sfb[kKcPar];
+    const uint64_t s = blockIdx.x;
+    const int lane = (int)threadIdx.x;
+    if (s >= A.count) return;
+    if (A.spec_mode != 0 && A.spec[s].flags != 0) return;
+    uint32_t *si = B.sinfo + kKcInfo * s;
+    if (pass > 1 && si[1] != kKcFailJudge) return;
+    const uint64_t c0 = s * (uint64_t)B.kmax;
+    const int32_t n = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+    const int32_t from0 = A.spec_mode != 0 ? (int32_t)A.spec[s].from : 0;
+    // the stream's chunks (present from 0 on, up to the one marked last) and their errors
+    int32_t K = B.kmax;
+    bool cerr = false;
+    for (int32_t k = lane; k < B.kmax; k += 64) {
+        const uint32_t f = B.meta[c0 + k].y;
+        const int32_t kk = !(f & kKcHave) ? k : ((f & kKcLast) ? k + 1 : B.kmax);
+        K = kk < K ? kk : K;
+    }
+    for (int d = 32; d >= 1; d >>= 1) {
+        const int32_t o = __shfl_xor(K, d, 64);
+        K = o < K ? o : K;
+    }
+    for (int32_t k = lane; k < K; k += 64) cerr = cerr || (B.meta[c0 + k].y & (kKcErr | kKcBad)) != 0;
+    uint32_t fail = __ballot(cerr) != 0 ? kKcFailChunk : 0u;
+    int32_t nseg = 0;
+    uint32_t tot = 0;
+    bool par = !fail && K <= kKcPar;
+    if (par) {
+        for (int32_t k = lane; k < K - 1; k += 64) {  // boundary k -> k+1
+            const uint32_t no = B.meta[c0 + k].x;
+            const uint4 *ro = B.crec + (c0 + k) * (uint64_t)B.rcap_c;
+            const int32_t bj = (int32_t)((int64_t)from0 + (int64_t)(k + 1) * B.C);
+            const uint4 mj = B.meta[c0 + k + 1];
+            const uint4 *rj = B.crec + (c0 + k + 1) * (uint64_t)B.rcap_c;
+            uint32_t fa = 0, fb = kKcNoJoin;
+            int32_t Q = 0;
+            if (mj.w != kKcNone) {
+                const uint32_t ia = kc_lower(ro, 0, no, (int32_t)mj.w);
+                if (ia < no && kc_nx(ro[ia]) == (int32_t)mj.w) fa = ia, fb = kKcVirt, Q = (int32_t)mj.w;
+            }
+            if (fb == kKcNoJoin) {
+                uint32_t ia = kc_lower(ro, 0, no, bj), ib = 0;
+                while (ia < no && ib < mj.x) {
+                    const int32_t va = kc_nx(ro[ia]), vb = kc_nx(rj[ib]);
+                    if (va == vb) {
+                        fa = ia, fb = ib, Q = va;
+                        break;
+                    }
+                    if (va < vb) ia++;
+                    else ib++;
+                }
+            }
+            sQ[k] = Q, sfa[k] = fa, sfb[k] = fb;
+        }
+        __syncthreads();
+        // every boundary joined, the joins increasing, each segment at least its start record
+        bool bad = false;
+        for (int32_t k = lane; k < K - 1; k += 64) {
+            if (sfb[k] == kKcNoJoin) bad = true;
+            else if (k > 0 && (sQ[k] <= sQ[k - 1] || sfb[k - 1] == kKcNoJoin ||
+                               (sfb[k - 1] != kKcVirt && sfa[k] < sfb[k - 1] + 1)))
+                bad = true;
+        }
+        par = __ballot(bad) == 0;
+    }
+    if (par) {
+        // segment k = chunk k: [Q_k-1, Q_k), records [ri_k, fa_k + 1), log [li_k, li of fa_k)
+        uint32_t *seg = B.seg + c0 * kKcSegWords;
+        uint32_t carry = 0;
+        for (int32_t k0 = 0; k0 < K; k0 += 64) {
+            const int32_t k = k0 + lane;
+            uint32_t cnt = 0, w[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            if (k < K) {
+                const uint4 mk = B.meta[c0 + k];
+                const uint4 *rk = B.crec + (c0 + k) * (uint64_t)B.rcap_c;
+                const bool first = k == 0, lastk = k == K - 1;
+                const bool pv = !first && sfb[k - 1] == kKcVirt;
+                const uint32_t ri = first || pv ? 0u : sfb[k - 1] + 1;
+                const uint32_t li = first || pv ? 0u : kc_li(rk[sfb[k - 1]]);
+                const uint32_t rhi = lastk ? mk.x : sfa[k] + 1;
+                const uint32_t lhi = lastk ? mk.z : kc_li(rk[sfa[k]]);
+                w[0] = (uint32_t)k, w[1] = first ? (uint32_t)from0 : (uint32_t)sQ[k - 1], w[2] = lastk ? (uint32_t)n : (uint32_t)sQ[k];
+                w[3] = ri, w[4] = rhi, w[6] = li, w[7] = lhi;
+                cnt = rhi - ri;
+            }
+            uint32_t incl = cnt;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t u = (uint32_t)__shfl_up((int)incl, d, 64);
+                if (lane >= d) incl += u;
+            }
+            if (k < K) {
+                w[5] = carry + incl - cnt;
+                for (int t = 0; t < kKcSegWords; t++) seg[(uint64_t)k * kKcSegWords + t] = w[t];
+            }
+            carry += (uint32_t)__shfl((int)incl, 63, 64);
+        }
+        nseg = K;
+        tot = carry;
+    } else if (!fail && lane == 0) {
+        fail = kc_stitch_seq(A, B, s, K, from0, n, nseg, tot);
+    }
+    fail = (uint32_t)__shfl((int)fail, 0, 64);
     if (!fail && tot > rcap) fail = kKcFailCap;
-    si[0] = (uint32_t)nseg;
-    si[1] = fail;
-    si[2] = (uint32_t)K;
-    si[3] = kKcNone;
-    si[4] = (uint32_t)pass;
-    for (int32_t k = 0; k < K; k++) B.cstart[c0 + k] = -1, B.cfail[c0 + k] = 0;  // (kc_v2 sets the segments' owners)
-    if (!fail) A.out_size[s] = tot;
+    for (int32_t k = lane; k < K; k += 64) B.cstart[c0 + k] = -1, B.cfail[c0 + k] = 0;  // (kc_v2 sets the segments' owners)
+    if (lane == 0) {
+        si[0] = (uint32_t)nseg;
+        si[1] = fail;
+        si[2] = (uint32_t)K;
+        si[3] = kKcNone;
+        si[4] = (uint32_t)pass;
+        if (!fail) A.out_size[s] = tot;
+    }
 }
 
 // streams still failed on a judgement after this pass (the host stops the passes at 0)
@@ -3040,7 +3138,7 @@ static hipError_t launch_chunk(const CompressArgs &a, uint8_t *recs, hipStream_t
         if (lw) hipLaunchKernelGGL(kc_parse<true>, dim3(pgrid), dim3(64), lds, st, a, B, pass);
         else hipLaunchKernelGGL(kc_parse<false>, dim3(pgrid), dim3(64), lds, st, a, B, pass);
         if ((e = hipGetLastError()) != hipSuccess) return e;
-        hipLaunchKernelGGL(kc_stitch, dim3((unsigned)((a.count + 63) / 64)), dim3(64), 0, st, a, B, rcap, pass);
+        hipLaunchKernelGGL(kc_stitch, dim3((unsigned)a.count), dim3(64), 0, st, a, B, rcap, pass);
         hipLaunchKernelGGL(kc_gather, dim3((unsigned)nc), dim3(256), 0, st, a, B, (uint4 *)recs, rcap, pass);
         hipLaunchKernelGGL(kc_v1, dim3((unsigned)nc), dim3(64), (size_t)2 * (size_t)a.hs * 4, st, a, B, pass);
         hipLaunchKernelGGL(kc_v2, dim3((unsigned)((a.count * (uint64_t)a.hs + 255) / 256)), dim3(256), 0, st, a, B, pass);

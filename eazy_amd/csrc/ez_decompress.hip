@@ -338,6 +338,8 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     // chip (C4s, 64 x 4 MiB: K2t 93.7 ms, K2j 11.4 ms; a lone 16 MiB log stream 171 / 11.7 ms).
     // Literal-heavy buckets stay on K2t (C4 fp32 0.149 / 1.86 ms, C4h 0.31 / 2.65 ms), and so do
     // batches of more streams, whose chains K2t runs side by side (1,024 x 1 MiB: 12.9 / 58.8 ms).
+    // K2j's time follows the batch's output, K2t's the longest stream's (256 x 1 MiB logs: K2t's
+    // chain ~12.8 ms against K2j 15.6): K2j only while the output is at most 200 slots' worth.
     if (v == 't' && !a.force && g_decompress_variant == 0 && a.count <= 256 && a.max_out >= ((uint64_t)1 << 20)) {
         uint64_t ext[4] = {0, 0, 0, 0};  // (the offsets may be a view into a larger batch's: absolute)
         if ((e = hipMemcpyAsync(&ext[0], a.in_off, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
@@ -346,7 +348,7 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
         if ((e = hipMemcpyAsync(&ext[3], a.out_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
         const uint64_t nin = ext[1] - ext[0], nout = ext[3] - ext[2];
-        if (nin >= (uint64_t)a.count * (64 << 10) && nout >= 2 * nin) v = 'j';
+        if (nin >= (uint64_t)a.count * (64 << 10) && nout >= 2 * nin && nout <= 200 * a.max_out) v = 'j';
     }
     if (v == 'j' && !jump_applies(a)) v = 't';
     g_last_variant = v;
