@@ -2284,8 +2284,15 @@ template <bool WIDE>
 __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
                                             uint64_t *stage = nullptr);
 
+// waves per SIMD the VGPR budget is cut for: 8-lane groups are held to ~2 by their tables' LDS, so
+// they keep VGPRs (no spills); (EZ_EXP & 8192 builds: 16-lane groups at 4, A/B)
+#if (EZ_EXP & 8192)
+constexpr int kLeanWaves16 = 4;
+#else
+constexpr int kLeanWaves16 = 5;
+#endif
 template <int TB, bool LW = false, int FW = 24, bool PERSIST = false, int G = 16>
-__global__ __launch_bounds__(64, TB == 12 ? 6 : 5) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
+__global__ __launch_bounds__(64, G == 8 ? 2 : (TB == 12 ? 6 : kLeanWaves16)) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                  uint64_t rcap, int prio, uint8_t *edge) {
     constexpr int S = 64 / G;
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -2794,6 +2801,7 @@ hipError_t launch_lean_v(const CompressArgs &a, uint64_t *recs, uint32_t stride,
     return hipGetLastError();
 }
 
+static uint32_t w12_words(const CompressArgs &a) { return (uint32_t)((2 * ((a.hs + 4) / 5) + 3) & ~3ll); }  // u32 words of a 12-bit table
 hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     // the visit by one ds_mskor (when its lane order holds); EZ_K1S_MSK=0 takes the DPP search (A/B).
     // EZ_K1S_T12=1 (A/B) puts streams of <= 4099 bytes on 12-bit tables: 6 waves per SIMD instead of
@@ -2807,8 +2815,8 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     // the waves, C1 measured 2.01 -> 2.14 ms, 8 KiB streams 8.58 -> 8.11, 16 KiB 11.06 -> 9.49 (with
     // the 40-byte judgement), 64 KiB 14.10 -> 11.67.  EZ_K1S_G=8 / 16 (A/B) forces one
     static const int gw = knob("EZ_K1S_G", 0);
-    const bool g8 = (gw == 8 || (gw == 0 && a.max_len > 4096)) && !t12 && msk && knob("EZ_K1S_LW", 1) != 0 &&
-                    split_stride<8, true>(a) != 0;
+    const bool g8 = (gw == 8 || (gw == 0 && a.max_len > 4096)) && msk && knob("EZ_K1S_LW", 1) != 0 &&
+                    (t12 ? (uint64_t)w12_words(a) * 4 * 8 <= 160 * 1024 : split_stride<8, true>(a) != 0);
     const int S = g8 ? 8 : 4;
     const uint32_t w12 = (uint32_t)((2 * ((a.hs + 4) / 5) + 3) & ~3ll);  // u32 words of a 12-bit table
     const uint32_t stride = t12 ? w12 : split_stride<16, true>(a), tw = t12 ? w12 : split_table_words<true>(a);
@@ -2837,7 +2845,8 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     const size_t lds = (size_t)stride * 4 * S + (lw && msk ? (size_t)kWinLdsBytes * S : 0) + pad;
     hipError_t e;
     if (g8) {
-        if (w40) e = launch_lean_v<16, true, 40, 8>(a, recs, stride, tw, lds, prio, edge, persist, st);
+        if (t12) e = launch_lean_v<12, true, 40, 8>(a, recs, stride, tw, lds, prio, edge, persist, st);
+        else if (w40) e = launch_lean_v<16, true, 40, 8>(a, recs, stride, tw, lds, prio, edge, persist, st);
         else e = launch_lean_v<16, true, 24, 8>(a, recs, stride, tw, lds, prio, edge, persist, st);
     } else if (lw && msk) {
         if (t12) e = launch_lean_v<12, true, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
