@@ -155,10 +155,10 @@ def load_traffic(path, workload, count, size, dom):
     else:
         t = json.load(open(path))
     kern = t.get("kernels", t)
-    # the stage's kernels: K1 = the parses and writers (k1_*) and K1x's rounds (kx_*); K2 = the decoders
-    # (k2_*) and the deferred-literal copy (kd_copy); K3 = k3_*; per step (a kernel a step runs several
-    # times counts every dispatch)
-    pre = {"k1_compress": ("k1_", "kx_"), "k2_decompress": ("k2_", "kd_"), "k3_pack": ("k3_",)}[dom]
+    # the stage's kernels: K1 = the parses and writers (k1_*), K1x's rounds (kx_*), K1c's chunks (kc_*)
+    # and the wide token writer (ke_*); K2 = the decoders (k2_*), K2j (kj_*) and the deferred-literal
+    # copy (kd_copy); K3 = k3_*; per step (a kernel a step runs several times counts every dispatch)
+    pre = {"k1_compress": ("k1_", "kx_", "kc_", "ke_"), "k2_decompress": ("k2_", "kd_", "kj_"), "k3_pack": ("k3_",)}[dom]
     # (per_step is null in a profile without a k3_gather dispatch to count steps by: the per-launch figure)
     def stage(key, per):
         vals = [v[per] if v.get(per) is not None else v.get(key) for k, v in kern.items() if k.startswith(pre) and v.get(key)]

@@ -28,9 +28,10 @@ def main():
     L = ez._lib()
     src = synth.logs(91, 64 << 20).tobytes()
     res = {}
-    # warm-up Reader (first use of the K2j and K2t code objects, the shared K2j workspace, the pinned
-    # staging window) so that the first size's rate is not the process's one-time setup
-    wr = ez.NewReaderBytes(orc.compress(1 << 20, 1024, [src[: 64 << 10]]))
+    # warm-up Reader (first use of the K2j and K2t code objects, the pinned staging window, and the
+    # per-device K2j workspace sized for the largest stream below, 8 MiB) so that the first size's
+    # rate is not the process's one-time setup
+    wr = ez.NewReaderBytes(orc.compress(1 << 20, 1024, [src[: 8 << 20]]))
     while wr.Read(4096)[1] == ez.OK:
         pass
     for size in (100, 400, 1024, 4096):

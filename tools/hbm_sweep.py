@@ -11,7 +11,8 @@ import os
 import sys
 
 PEAK = 8000.0
-STAGES = {"k1_compress": ("k1_", "kx_"), "k3_pack": ("k3_",), "k2_decompress": ("k2_", "kd_")}  # kx_: K1x rounds, kd_: K2w deferred literals
+# kx_: K1x rounds, kc_: K1c chunks, ke_: the wide token writer, kd_: deferred literals, kj_: K2j
+STAGES = {"k1_compress": ("k1_", "kx_", "kc_", "ke_"), "k3_pack": ("k3_",), "k2_decompress": ("k2_", "kd_", "kj_")}
 
 
 def main():
