@@ -420,3 +420,40 @@ def test_multi_device_batches_equal_one_device(cuda):
     if lens[1] > 0:
         out, sizes, st = ez.decompress_batch_multi(packed, poff, out_off[:3], devices=[0, 0])
         assert st[0] == 0 and st[1] != 0
+
+
+@pytest.mark.gpu
+def test_c1_full_batch_matches_oracle(cuda):
+    """C1 at its full size (BASELINE.json configs[1]): 65,536 x 4 KiB synthetic log streams,
+    NewWriter(MiB, 1024).Write(p) each (writer.go:133, :206). Every stream's bytes, packed, equal
+    the C oracle's (oracle/eazy_oracle.c, 16 threads), and the automatic K2 decodes them all back on
+    the device. The other tests in this file cover the edge shapes on a few hundred streams; this one
+    runs the headline batch itself, through the same C-ABI calls bench.py times."""
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    n, S = 4096, 65536
+    host = synth.logs(2025, n * S)
+    offs = np.arange(S + 1, dtype=np.int64) * n
+    cap = n + (n >> 2) + 64
+    slot_off = np.arange(S + 1, dtype=np.int64) * cap
+    slots, sizes = orc.compress_batch(MiB, 1024, host, offs, slot_off, 16)
+    want = slots.reshape(S, cap)
+    data = torch.from_numpy(host).to(cuda)
+    off = torch.from_numpy(offs).to(cuda)
+    cb = ez.compress_batch(data, off, MiB, 1024, append_magic=True)
+    packed, poff = ez.pack(cb)
+    torch.cuda.synchronize()
+    assert int(cb.status.count_nonzero()) == 0
+    po = poff.cpu().numpy()
+    assert np.array_equal(np.diff(po), sizes), "compressed sizes differ from the oracle's"
+    pk = packed[: int(po[-1])].cpu().numpy()
+    # every stream's bytes: the packed stream s against the oracle's slot s
+    keep = np.arange(cap)[None, :] < sizes[:, None]
+    assert np.array_equal(pk, want[keep]), "compressed bytes differ from the oracle's"
+    out, osz, ost = ez.decompress_batch(packed, poff, off, max_len=n)
+    torch.cuda.synchronize()
+    assert int(ost.count_nonzero()) == 0 and bool((osz == n).all())
+    assert torch.equal(out[: n * S], data), "round trip differs"
