@@ -497,3 +497,73 @@ def test_k2j_chip_wide_decode(cuda):
                     continue
                 n = int(sz[i])
                 assert int(st[i]) == err and o[ooff[i] : ooff[i] + n].tobytes() == want, (k, n)
+
+
+@pytest.mark.gpu
+def test_c2_full_batch_matches_oracle(cuda):
+    """C2 at its full size (BASELINE.json configs[2]): 4,096 x 256 KiB synthetic log streams
+    into NewWriter(MiB, 1024), the automatic route (K1L + its token writer, K3, K2t). Every
+    stream's packed bytes equal the C oracle's (16 threads) and decode back on the device."""
+    import torch
+
+    import eazy_amd as ez
+    from eazy_amd import synth
+
+    n, S = 256 << 10, 4096
+    host = synth.logs(2026, n * S)
+    offs = np.arange(S + 1, dtype=np.int64) * n
+    cap = n + (n >> 2) + 64
+    slot_off = np.arange(S + 1, dtype=np.int64) * cap
+    slots, sizes = orc.compress_batch(MiB, 1024, host, offs, slot_off, 16)
+    data = torch.from_numpy(host).to(cuda)
+    off = torch.from_numpy(offs).to(cuda)
+    cb = ez.compress_batch(data, off, MiB, 1024, append_magic=True)
+    packed, poff = ez.pack(cb)
+    torch.cuda.synchronize()
+    assert int(cb.status.count_nonzero()) == 0
+    po = poff.cpu().numpy()
+    assert np.array_equal(np.diff(po), sizes), "compressed sizes differ from the oracle's"
+    pk = packed[: int(po[-1])].cpu().numpy()
+    keep = np.arange(cap)[None, :] < sizes[:, None]
+    assert np.array_equal(pk, slots.reshape(S, cap)[keep]), "compressed bytes differ from the oracle's"
+    del slots, keep
+    out, osz, ost = ez.decompress_batch(packed, poff, off, max_len=n)
+    torch.cuda.synchronize()
+    assert int(ost.count_nonzero()) == 0 and bool((osz == n).all())
+    assert torch.equal(out[: n * S], data), "round trip differs"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wl", ["c4", "c4h", "c4s"])
+def test_c4_full_batches_match_oracle(cuda, wl):
+    """C4 at its full size (BASELINE.json configs[4]): 64 x 4 MiB gradient buckets bit-cast to bytes
+    (fp32 N(0, 1e-3); its bf16 top halves; fp32 with 90 % zeros), the bench's own bytes
+    (bench.workload_bytes), the automatic route (K1x's rounds, then K1c or K1L; K2t or K2j). Every
+    stream's packed bytes equal the C oracle's and decode back on the device."""
+    import torch
+
+    import bench
+    import eazy_amd as ez
+
+    S, n = 64, 4 << 20
+    host, _ = bench.workload_bytes(wl, 7, S * n)
+    host = np.ascontiguousarray(host)
+    offs = np.arange(S + 1, dtype=np.int64) * n
+    cap = n + (n >> 2) + 64
+    slot_off = np.arange(S + 1, dtype=np.int64) * cap
+    slots, sizes = orc.compress_batch(MiB, 1024, host, offs, slot_off, 16)
+    data = torch.from_numpy(host).to(cuda)
+    off = torch.from_numpy(offs).to(cuda)
+    cb = ez.compress_batch(data, off, MiB, 1024, append_magic=True)
+    packed, poff = ez.pack(cb)
+    torch.cuda.synchronize()
+    assert int(cb.status.count_nonzero()) == 0
+    po = poff.cpu().numpy()
+    assert np.array_equal(np.diff(po), sizes), f"{wl}: compressed sizes differ from the oracle's"
+    pk = packed[: int(po[-1])].cpu().numpy()
+    keep = np.arange(cap)[None, :] < sizes[:, None]
+    assert np.array_equal(pk, slots.reshape(S, cap)[keep]), f"{wl}: compressed bytes differ from the oracle's"
+    out, osz, ost = ez.decompress_batch(packed, poff, off, max_len=n)
+    torch.cuda.synchronize()
+    assert int(ost.count_nonzero()) == 0 and bool((osz == n).all())
+    assert torch.equal(out[: n * S], data), f"{wl}: round trip differs"
