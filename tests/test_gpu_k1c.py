@@ -154,3 +154,14 @@ def test_wide_token_writer_small_slots(cuda, count):
             if c >= 9:
                 assert int(sizes[k]) > 0, k
     del slot
+
+
+def test_k1c_full_1mib_batch(cuda):
+    """The sweep's 1 MiB line at its full size: 1,024 x 1 MiB log Writes (longer than half the
+    window: K1x's rounds hand the dense streams over, then K1c with its passes, K1L for what it
+    cannot prove). Every stream equal to the oracle, decoded back; most proven by K1c itself."""
+    d = _logs(67, 1024 * MiB)
+    bufs = [d[k * MiB : (k + 1) * MiB] for k in range(1024)]
+    st = _compress(cuda, bufs)
+    assert st["proven"] + st["chunk"] + st["sync"] + st["judge"] + st["cap"] == 1024, st
+    assert st["proven"] >= 512, st
