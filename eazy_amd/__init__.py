@@ -190,6 +190,23 @@ def k1c_stats(enable: bool) -> dict:
     return dict(zip(("proven", "chunk", "sync", "judge", "cap", "segments"), (int(v) for v in out)))
 
 
+def release_cached(device: int = -1) -> None:
+    """ez_release_cached: free the device scratch kept between batch calls (device < 0: all)."""
+    _check(_lib().ez_release_cached(device))
+
+
+def multi_last_shards() -> list:
+    """ez_multi_last_shards: [(device, t0_ms, t1_ms)] of the last multi-device batch call's shards."""
+    L = _lib()
+    L.ez_multi_last_shards.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int]
+    n = L.ez_multi_last_shards(None, None, None, 0)
+    dev = (C.c_int * max(n, 1))()
+    t0 = (C.c_double * max(n, 1))()
+    t1 = (C.c_double * max(n, 1))()
+    n = L.ez_multi_last_shards(dev, t0, t1, n)
+    return [(dev[k], t0[k], t1[k]) for k in range(n)]
+
+
 def _check(code: int, detail: int = 0) -> None:
     if code == OK:
         return
@@ -442,6 +459,7 @@ class Reader:
         _lib().ez_reader_set_whole(h, 0 if r is not None else 1)  # a whole buffer: decoded at once
         self.Reader = r
         self._b = bytearray(b or b"")
+        self._bcap = len(self._b)  # cap(r.b)
         self._i = 0
         self._boff = 0
         self.BlockSizeLimit = 16 * MiB if r is not None else 0
@@ -463,6 +481,7 @@ class Reader:
     def ResetBytes(self, b: bytes) -> None:  # reader.go:102-113
         self.Reader = None
         self._b = bytearray(b)
+        self._bcap = len(self._b)
         self._i = 0
         self._boff = 0
         _lib().ez_reader_reset(self._h)
@@ -505,7 +524,12 @@ class Reader:
         del self._b[: self._i]
         self._boff += self._i
         self._i = 0
-        room = self.BufferSize if not self._b else 1024
+        end = len(self._b)
+        if end == 0:  # r.b = make([]byte, r.BufferSize)
+            self._bcap = self.BufferSize
+        else:  # r.b = append(r.b, make([]byte, 1024)...): the same array unless it has no room
+            self._bcap = _go_append_cap(self._bcap, end + 1024)
+        room = self._bcap - end  # r.Reader.Read(r.b[end:cap(r.b)])
         if hasattr(self.Reader, "read_go"):
             data, err = self.Reader.read_go(room)
         else:
@@ -515,6 +539,34 @@ class Reader:
         if data and err == EOF:
             err = OK
         return err
+
+
+# Go's size classes (runtime/sizeclasses.go) and growslice for a byte slice (runtime/slice.go, Go 1.20,
+# the reference's go.mod): the capacity append(r.b, make([]byte, 1024)...) leaves in more()
+# (reader.go:529), which decides how much the next io.Reader.Read is offered.
+_GO_CLASSES = (8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 144, 160, 176, 192, 208, 224, 240, 256, 288, 320, 352, 384, 416,
+               448, 480, 512, 576, 640, 704, 768, 896, 1024, 1152, 1280, 1408, 1536, 1792, 2048, 2304, 2688, 3072, 3200,
+               3456, 4096, 4864, 5376, 6144, 6528, 6784, 6912, 8192, 9472, 9728, 10240, 10880, 12288, 13568, 14336,
+               16384, 18432, 19072, 20480, 21760, 24576, 27264, 28672, 32768)
+
+
+def _go_append_cap(old_cap: int, new_len: int) -> int:
+    """cap(append(s, ...)) for a []byte of capacity old_cap grown to new_len elements."""
+    if new_len <= old_cap:
+        return old_cap
+    newcap = old_cap
+    if new_len > 2 * old_cap:
+        newcap = new_len
+    elif old_cap < 256:
+        newcap = 2 * old_cap
+    else:
+        while 0 < newcap < new_len:
+            newcap += (newcap + 3 * 256) // 4
+        if newcap <= 0:
+            newcap = new_len
+    if newcap < 32768:  # roundupsize: the smallest size class, else whole 8 KiB pages
+        return next(c for c in _GO_CLASSES if c >= newcap) if newcap > 0 else 0
+    return (newcap + 8191) & ~8191
 
 
 def NewReader(r, device: int = 0) -> Reader:
@@ -538,6 +590,8 @@ class _Batch(C.Structure):
         ("status", C.c_void_p),
         ("count", C.c_uint64),
         ("max_len", C.c_uint64),
+        ("in_bytes", C.c_uint64),   # decompress hints (ABI 2): the batch's input / output extents
+        ("out_bytes", C.c_uint64),
     ]
 
 
@@ -708,10 +762,14 @@ def pack(cb: CompressedBatch, packed=None, packed_off=None, workspace=None, stre
 
 
 def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=None, sizes=None, status=None,
-                     workspace=None, exact_only: bool = False, stream=None, max_len: int = 0):
+                     workspace=None, exact_only: bool = False, stream=None, max_len: int = 0,
+                     in_bytes: int = 0, out_bytes: int = 0):
     """K2: decode complete streams comp[comp_off[s]:comp_off[s+1]] into
     out[out_off[s]:out_off[s+1]] -> (out, sizes, status).  exact_only skips
-    the fast decoders (every stream on the exact decoder)."""
+    the fast decoders (every stream on the exact decoder).  max_len (the largest
+    slot), in_bytes = comp_off[-1] - comp_off[0] and out_bytes = out_off[-1] -
+    out_off[0] are optional host hints: with them the call never waits for the
+    stream to pick its decoder."""
     import torch
 
     _need_cuda(comp, comp_off, out_off)
@@ -726,7 +784,7 @@ def decompress_batch(comp, comp_off, out_off, block_size_limit: int = 0, out=Non
     if workspace is None and not exact_only:
         workspace = torch.empty(_lib().ez_decompress_workspace(count), dtype=torch.uint8, device=dev)
     b = _Batch(comp.data_ptr(), comp_off.data_ptr(), out.data_ptr(), out_off.data_ptr(), sizes.data_ptr(),
-               status.data_ptr(), count, max_len)
+               status.data_ptr(), count, max_len, in_bytes, out_bytes)
     ws = None if exact_only else workspace.data_ptr()
     _check(_lib().ez_decompress_batch(block_size_limit, C.byref(b), ws, _stream_ptr(stream)))
     return out, sizes, status

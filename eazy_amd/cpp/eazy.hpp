@@ -351,6 +351,7 @@ class Reader {
     void ResetBytes(const uint8_t *b, size_t n) {  // reader.go:102-113
         R = nullptr;
         b_.assign(b, b + n);
+        bcap_ = n;
         i_ = 0;
         boff_ = 0;
         ez_reader_reset(h_);
@@ -390,8 +391,29 @@ class Reader {
   private:
     ez_reader *h_ = nullptr;
     std::vector<uint8_t> b_;  // r.b
+    size_t bcap_ = 0;         // cap(r.b)
     size_t i_ = 0;            // r.i
     int64_t boff_ = 0;        // r.boff
+
+    // cap(append(s, ...)) for a []byte of capacity c grown to n elements: Go 1.20's growslice and
+    // roundupsize (runtime/slice.go, runtime/sizeclasses.go; the reference's go.mod)
+    static size_t go_append_cap(size_t c, size_t n) {
+        if (n <= c) return c;
+        size_t nc = c;
+        if (n > 2 * c) nc = n;
+        else if (c < 256) nc = 2 * c;
+        else
+            while (nc < n) nc += (nc + 3 * 256) / 4;
+        static const uint16_t cls[] = {8, 16, 24, 32, 48, 64, 80, 96, 112, 128, 144, 160, 176, 192, 208, 224, 240, 256, 288, 320, 352, 384, 416,
+                                       448, 480, 512, 576, 640, 704, 768, 896, 1024, 1152, 1280, 1408, 1536, 1792, 2048, 2304, 2688, 3072, 3200,
+                                       3456, 4096, 4864, 5376, 6144, 6528, 6784, 6912, 8192, 9472, 9728, 10240, 10880, 12288, 13568, 14336,
+                                       16384, 18432, 19072, 20480, 21760, 24576, 27264, 28672, 32768};
+        if (nc < 32768) {
+            for (uint16_t k : cls)
+                if (k >= nc) return k;
+        }
+        return (nc + 8191) & ~(size_t)8191;
+    }
 
     Err more() {  // reader.go:516-543
         if (!R) return Err::EOF_;
@@ -399,7 +421,10 @@ class Reader {
         boff_ += (int64_t)i_;
         i_ = 0;
         const size_t end = b_.size();
-        b_.resize(end + (end == 0 ? (size_t)BufferSize : 1024));
+        // r.b = make([]byte, r.BufferSize), or append(r.b, make([]byte, 1024)...) in the same array
+        // while it has room: the io.Reader is offered r.b[end:cap(r.b)]
+        bcap_ = end == 0 ? (size_t)BufferSize : go_append_cap(bcap_, end + 1024);
+        b_.resize(bcap_);
         auto [k, err] = R->Read(b_.data() + end, b_.size() - end);
         b_.resize(end + k);
         if (k != 0 && err == Err::EOF_) err = Err::OK;
@@ -667,6 +692,9 @@ inline Err CompressBatch(int64_t block, int64_t htable, bool append_magic, const
     }
     return (Err)st;
 }
+// ez_release_cached: the device scratch kept between batch calls freed (device < 0: every device)
+inline Err ReleaseCached(int device = -1) { return (Err)ez_release_cached(device); }
+
 inline Err DecompressBatch(int64_t block_size_limit, const ez_batch &b, void *workspace, void *hip_stream) {
     return (Err)ez_decompress_batch(block_size_limit, &b, workspace, hip_stream);
 }

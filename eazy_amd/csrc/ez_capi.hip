@@ -16,6 +16,7 @@
 #include <memory>
 #include <thread>
 
+#include "ez_cache.h"
 #include "ez_format.h"
 #include "ez_internal.h"
 
@@ -100,12 +101,13 @@ size_t header_bytes(uint8_t *b, int append_magic, int ver, int64_t bs) {
     return k;
 }
 
-// K1 scratch (match records / global hash tables), one per (device, HIP stream):
-// batch calls on distinct streams may run concurrently (SURVEY §8b threading)
-struct Scratch {
-    DBuf ht;
-};
-std::map<std::pair<int, void *>, Scratch> g_scratch;
+// K1 scratch (match records / global hash tables / K1c's logs), one per (device, HIP stream), each
+// locked only by the call using it: batch calls on distinct streams run concurrently (SURVEY §8b
+// threading; ez_cache.h)
+ez::DevCache &k1_cache() {
+    static ez::DevCache *c = new ez::DevCache();  // (never destroyed: no hipFree after the runtime's teardown)
+    return *c;
+}
 
 }  // namespace
 
@@ -1010,17 +1012,24 @@ static int compress_batch_impl(int64_t block, int64_t htable, int flags, const e
     // general kernel (one wave per stream, the history read from the stream's earlier Writes)
     if (write_idx && b->count == 0) return EZ_OK;
     const bool split_mw = write_idx && ez::split_stride_words(a) != 0;
-    const uint64_t words = split_mw ? ez::split_scratch_words(a) : ez::compress_scratch_words(a);
-    // the scratch of this (device, stream) stays locked through the launches: another host thread
+    auto words_of = [&](const ez::CompressArgs &x) { return split_mw ? ez::split_scratch_words(x) : ez::compress_scratch_words(x); };
+    uint64_t words = words_of(a);
+    // the scratch of this (device, stream) stays leased through the launches: another host thread
     // growing it meanwhile would free what these kernels were given
-    std::unique_lock<std::mutex> lk(g_mu, std::defer_lock);
+    ez::CacheLease lease;
     if (words) {
         int dev = 0;
         EZ_HIP(hipGetDevice(&dev));
-        lk.lock();
-        Scratch &sc = g_scratch[std::make_pair(dev, hip_stream)];
-        if (sc.ht.ensure((size_t)words * 4)) return EZ_EDEVICE;
-        a.ht_global = sc.ht.as<uint32_t>();
+        lease = k1_cache().acquire(dev, hip_stream);
+        if (!lease->ensure((size_t)words * 4)) {
+            // K1c's logs (about 13 bytes per input byte) may not fit where K1L's records do: K1L alone
+            ez::CompressArgs b = a;
+            b.no_k1c = 1;
+            const uint64_t w2 = words_of(b);
+            if (w2 >= words || !lease->ensure((size_t)w2 * 4)) return EZ_EDEVICE;
+            a = b;
+        }
+        a.ht_global = (uint32_t *)lease->p;
     }
     if (split_mw) EZ_HIP(ez::launch_compress_split(a, a.ht_global, (hipStream_t)hip_stream));
     else EZ_HIP(ez::launch_compress(a, (hipStream_t)hip_stream));
@@ -1097,6 +1106,8 @@ extern "C" int ez_decompress_batch(int64_t block_size_limit, const ez_batch *b, 
     a.handle = 0;
     a.slow = (uint32_t *)workspace;
     a.max_out = b->max_len;  // decompress: the largest output slot, if the caller knows it
+    a.in_bytes = b->in_bytes;  // the batch's extents, if the caller knows them
+    a.out_bytes = b->out_bytes;
     EZ_HIP(ez::launch_decompress(a, (hipStream_t)hip_stream));
     return EZ_OK;
 }
@@ -1133,24 +1144,91 @@ int resolve_devices(const int *devices, int ndev, std::vector<int> &out) {
     return EZ_OK;
 }
 
-// one shard's device buffers and HIP stream (its host thread owns them)
-struct Shard {
+// A shard's HIP stream, timing events and grow-only device buffers, pooled per device between calls:
+// the K1 / K2j scratch caches are keyed by (device, stream), so pooled streams reuse their entries
+// instead of leaving one behind per call, and repeated calls do not re-allocate (ez_release_cached
+// frees the idle ones).
+struct ShardRes {
     int dev = 0;
-    uint64_t first = 0, count = 0;
     hipStream_t st = nullptr;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;  // around the shard's device work
     DBuf in, in_off, out, out_off, size, status, ws, packed, packed_off;
-    uint64_t total = 0, base = 0;  // compress: packed bytes of the shard, its place in the global packing
-    int err = EZ_OK;
-    ~Shard() {
-        if (dev >= 0) (void)hipSetDevice(dev);
+    void release_bufs() {
         for (DBuf *b : {&in, &in_off, &out, &out_off, &size, &status, &ws, &packed, &packed_off}) b->release();
-        if (st) (void)hipStreamDestroy(st);
     }
 };
 
-// run f(shard) on one host thread per shard (each binds its device first) and join them
+class ShardPool {
+  public:
+    // an idle resource of dev, or a new one (the caller's thread is bound to dev); nullptr on failure
+    ShardRes *take(int dev) {
+        {
+            std::lock_guard<std::mutex> lk(m_);
+            auto &v = idle_[dev];
+            if (!v.empty()) {
+                ShardRes *r = v.back();
+                v.pop_back();
+                return r;
+            }
+        }
+        ShardRes *r = new ShardRes();
+        r->dev = dev;
+        if (hipStreamCreateWithFlags(&r->st, hipStreamNonBlocking) != hipSuccess || hipEventCreate(&r->ev0) != hipSuccess ||
+            hipEventCreate(&r->ev1) != hipSuccess) {
+            if (r->ev0) (void)hipEventDestroy(r->ev0);
+            if (r->st) (void)hipStreamDestroy(r->st);
+            delete r;
+            return nullptr;
+        }
+        return r;
+    }
+    void give(ShardRes *r) {
+        std::lock_guard<std::mutex> lk(m_);
+        idle_[r->dev].push_back(r);
+    }
+    // free the idle resources' buffers on dev (all devices for dev < 0); streams and events stay
+    void trim(int dev) {
+        std::lock_guard<std::mutex> lk(m_);
+        for (auto &kv : idle_) {
+            if (dev >= 0 && kv.first != dev) continue;
+            if (hipSetDevice(kv.first) != hipSuccess) continue;
+            for (ShardRes *r : kv.second) r->release_bufs();
+        }
+    }
+
+  private:
+    std::mutex m_;
+    std::map<int, std::vector<ShardRes *>> idle_;
+};
+ShardPool &shard_pool() {
+    static ShardPool *p = new ShardPool();  // (never destroyed: no HIP calls after the runtime's teardown)
+    return *p;
+}
+
+// one shard of a multi-device call (its host thread runs it on a pooled resource)
+struct Shard {
+    int dev = 0;
+    uint64_t first = 0, count = 0;
+    ShardRes *r = nullptr;
+    uint64_t total = 0, base = 0;  // compress: packed bytes of the shard, its place in the global packing
+    int err = EZ_OK;
+    ~Shard() {
+        if (r) shard_pool().give(r);
+    }
+};
+
+// the per-shard device intervals of the last multi-device call (ez_multi_last_shards)
+struct ShardTime {
+    int dev;
+    double t0, t1;
+};
+std::mutex g_times_mu;
+std::vector<ShardTime> g_times;
+
+// run f(shard) on one host thread per shard (each binds its device and takes a pooled resource
+// first), join them, then record their device intervals
 template <class F>
-int each_shard(std::vector<std::unique_ptr<Shard>> &sh, F f) {
+int each_shard(std::vector<std::unique_ptr<Shard>> &sh, F f, bool record = true) {
     std::vector<std::thread> th;
     for (auto &p : sh) {
         Shard *x = p.get();
@@ -1160,20 +1238,62 @@ int each_shard(std::vector<std::unique_ptr<Shard>> &sh, F f) {
                 x->err = EZ_EDEVICE;
                 return;
             }
-            if (!x->st && hipStreamCreateWithFlags(&x->st, hipStreamNonBlocking) != hipSuccess) {
-                x->st = nullptr;
+            if (!x->r && !(x->r = shard_pool().take(x->dev))) {
                 x->err = EZ_EDEVICE;
                 return;
             }
-            if (x->err == EZ_OK) x->err = f(*x);
+            if (x->err != EZ_OK) return;
+            if (hipEventRecord(x->r->ev0, x->r->st) != hipSuccess) {
+                x->err = EZ_EDEVICE;
+                return;
+            }
+            x->err = f(*x);
+            if (x->err == EZ_OK && (hipEventRecord(x->r->ev1, x->r->st) != hipSuccess || hipEventSynchronize(x->r->ev1) != hipSuccess))
+                x->err = EZ_EDEVICE;
         });
     }
     for (auto &t : th) t.join();
     for (auto &p : sh)
         if (p->err != EZ_OK) return p->err;
+    if (!record) return EZ_OK;
+    // device intervals, in ms from the earliest shard start on the same device
+    std::vector<ShardTime> tv;
+    for (auto &p : sh) {
+        if (!p->r || p->count == 0) continue;
+        const Shard *ref = nullptr;
+        for (auto &q : sh) {  // the shard on this device whose start is earliest
+            if (!q->r || q->count == 0 || q->dev != p->dev) continue;
+            if (!ref) {
+                ref = q.get();
+                continue;
+            }
+            float e = 0.f;
+            if (hipSetDevice(p->dev) == hipSuccess && hipEventElapsedTime(&e, ref->r->ev0, q->r->ev0) == hipSuccess && e < 0.f) ref = q.get();
+        }
+        float a = 0.f, b = 0.f;
+        if (hipSetDevice(p->dev) != hipSuccess || hipEventElapsedTime(&a, ref->r->ev0, p->r->ev0) != hipSuccess ||
+            hipEventElapsedTime(&b, ref->r->ev0, p->r->ev1) != hipSuccess)
+            a = b = -1.f;
+        tv.push_back(ShardTime{p->dev, (double)a, (double)b});
+    }
+    std::lock_guard<std::mutex> lk(g_times_mu);
+    g_times.swap(tv);
     return EZ_OK;
 }
 }  // namespace
+
+// Introspection (tests, measurement): the shards of the last multi-device call and their device
+// intervals (ms from the earliest shard start on the same device; -1 if not measurable)
+extern "C" int ez_multi_last_shards(int *dev, double *t0, double *t1, int cap) {
+    std::lock_guard<std::mutex> lk(g_times_mu);
+    const int n = (int)g_times.size();
+    for (int k = 0; k < n && k < cap; k++) {
+        if (dev) dev[k] = g_times[(size_t)k].dev;
+        if (t0) t0[k] = g_times[(size_t)k].t0;
+        if (t1) t1[k] = g_times[(size_t)k].t1;
+    }
+    return n;
+}
 
 #define EZ_SHARD_HIP(x)                          \
     do {                                         \
@@ -1211,26 +1331,26 @@ extern "C" int ez_compress_batch_multi(int64_t block, int64_t htable, int flags,
                 mx = n > mx ? n : mx;
                 ooff[t + 1] = ooff[t] + ((ez_compress_bound(n) + 15) & ~15ull);
             }
-            if (x.in.ensure(nb + 64) || x.in_off.ensure(8 * (c + 1)) || x.out.ensure(ooff[c] + 64) || x.out_off.ensure(8 * (c + 1)) ||
-                x.size.ensure(8 * c) || x.status.ensure(4 * c) || x.ws.ensure(ez_pack_workspace(c) + 64) || x.packed.ensure(ooff[c] + 64) ||
-                x.packed_off.ensure(8 * (c + 1)))
+            if (x.r->in.ensure(nb + 64) || x.r->in_off.ensure(8 * (c + 1)) || x.r->out.ensure(ooff[c] + 64) || x.r->out_off.ensure(8 * (c + 1)) ||
+                x.r->size.ensure(8 * c) || x.r->status.ensure(4 * c) || x.r->ws.ensure(ez_pack_workspace(c) + 64) || x.r->packed.ensure(ooff[c] + 64) ||
+                x.r->packed_off.ensure(8 * (c + 1)))
                 return EZ_EDEVICE;
-            if (nb) EZ_SHARD_HIP(hipMemcpyAsync(x.in.p, in + base, nb, hipMemcpyHostToDevice, x.st));
-            EZ_SHARD_HIP(hipMemcpyAsync(x.in_off.p, ioff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.st));
-            EZ_SHARD_HIP(hipMemcpyAsync(x.out_off.p, ooff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.st));
-            ez_batch b{x.in.as<uint8_t>(), x.in_off.as<uint64_t>(), x.out.as<uint8_t>(), x.out_off.as<uint64_t>(),
-                       x.size.as<uint64_t>(), x.status.as<int32_t>(), c, mx};
-            int r = ez_compress_batch(block, htable, flags, &b, x.st);
+            if (nb) EZ_SHARD_HIP(hipMemcpyAsync(x.r->in.p, in + base, nb, hipMemcpyHostToDevice, x.r->st));
+            EZ_SHARD_HIP(hipMemcpyAsync(x.r->in_off.p, ioff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.r->st));
+            EZ_SHARD_HIP(hipMemcpyAsync(x.r->out_off.p, ooff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.r->st));
+            ez_batch b{x.r->in.as<uint8_t>(), x.r->in_off.as<uint64_t>(), x.r->out.as<uint8_t>(), x.r->out_off.as<uint64_t>(),
+                       x.r->size.as<uint64_t>(), x.r->status.as<int32_t>(), c, mx};
+            int r = ez_compress_batch(block, htable, flags, &b, x.r->st);
             if (r != EZ_OK) return r;
-            r = ez_pack_batch(x.out.as<uint8_t>(), x.out_off.as<uint64_t>(), x.size.as<uint64_t>(), c, x.packed.as<uint8_t>(),
-                              x.packed_off.as<uint64_t>(), x.ws.p, x.st);
+            r = ez_pack_batch(x.r->out.as<uint8_t>(), x.r->out_off.as<uint64_t>(), x.r->size.as<uint64_t>(), c, x.r->packed.as<uint8_t>(),
+                              x.r->packed_off.as<uint64_t>(), x.r->ws.p, x.r->st);
             if (r != EZ_OK) return r;
             // the shard's packed offsets straight into the caller's array (rebased below; its last one,
             // the shard's total, is the next shard's first entry and comes back separately)
-            EZ_SHARD_HIP(hipMemcpyAsync(packed_off + x.first, x.packed_off.p, 8 * c, hipMemcpyDeviceToHost, x.st));
-            EZ_SHARD_HIP(hipMemcpyAsync(&x.total, x.packed_off.as<uint64_t>() + c, 8, hipMemcpyDeviceToHost, x.st));
-            if (status) EZ_SHARD_HIP(hipMemcpyAsync(status + x.first, x.status.p, 4 * c, hipMemcpyDeviceToHost, x.st));
-            EZ_SHARD_HIP(hipStreamSynchronize(x.st));
+            EZ_SHARD_HIP(hipMemcpyAsync(packed_off + x.first, x.r->packed_off.p, 8 * c, hipMemcpyDeviceToHost, x.r->st));
+            EZ_SHARD_HIP(hipMemcpyAsync(&x.total, x.r->packed_off.as<uint64_t>() + c, 8, hipMemcpyDeviceToHost, x.r->st));
+            if (status) EZ_SHARD_HIP(hipMemcpyAsync(status + x.first, x.r->status.p, 4 * c, hipMemcpyDeviceToHost, x.r->st));
+            EZ_SHARD_HIP(hipStreamSynchronize(x.r->st));
             return EZ_OK;
         });
         if (e != EZ_OK) return e;
@@ -1245,10 +1365,10 @@ extern "C" int ez_compress_batch_multi(int64_t block, int64_t htable, int flags,
         if (at > packed_cap) return EZ_ENOSPC;
         // phase 2: every shard's packed bytes down to its place
         return each_shard(sh, [&](Shard &x) -> int {
-            if (x.total) EZ_SHARD_HIP(hipMemcpyAsync(packed + x.base, x.packed.p, x.total, hipMemcpyDeviceToHost, x.st));
-            EZ_SHARD_HIP(hipStreamSynchronize(x.st));
+            if (x.total) EZ_SHARD_HIP(hipMemcpyAsync(packed + x.base, x.r->packed.p, x.total, hipMemcpyDeviceToHost, x.r->st));
+            EZ_SHARD_HIP(hipStreamSynchronize(x.r->st));
             return EZ_OK;
-        });
+        }, false);
     } catch (...) {
         return EZ_EDEVICE;  // (host allocation failure: nothing unwinds across the C-ABI)
     }
@@ -1282,24 +1402,47 @@ extern "C" int ez_decompress_batch_multi(int64_t block_size_limit, const uint8_t
                 ooff[t] = out_off[x.first + t] - ob;
                 if (t) mx = ooff[t] - ooff[t - 1] > mx ? ooff[t] - ooff[t - 1] : mx;
             }
-            if (x.in.ensure(nb + 64) || x.in_off.ensure(8 * (c + 1)) || x.out.ensure(no + 64) || x.out_off.ensure(8 * (c + 1)) ||
-                x.size.ensure(8 * c) || x.status.ensure(4 * c) || x.ws.ensure(ez_decompress_workspace(c) + 64))
+            if (x.r->in.ensure(nb + 64) || x.r->in_off.ensure(8 * (c + 1)) || x.r->out.ensure(no + 64) || x.r->out_off.ensure(8 * (c + 1)) ||
+                x.r->size.ensure(8 * c) || x.r->status.ensure(4 * c) || x.r->ws.ensure(ez_decompress_workspace(c) + 64))
                 return EZ_EDEVICE;
-            if (nb) EZ_SHARD_HIP(hipMemcpyAsync(x.in.p, in + ib, nb, hipMemcpyHostToDevice, x.st));
-            EZ_SHARD_HIP(hipMemcpyAsync(x.in_off.p, ioff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.st));
-            EZ_SHARD_HIP(hipMemcpyAsync(x.out_off.p, ooff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.st));
-            // (the largest slot given: the decoder route needs no device read-back)
-            ez_batch b{x.in.as<uint8_t>(), x.in_off.as<uint64_t>(), x.out.as<uint8_t>(), x.out_off.as<uint64_t>(),
-                       x.size.as<uint64_t>(), x.status.as<int32_t>(), c, mx ? mx : 1};
-            const int r = ez_decompress_batch(block_size_limit, &b, x.ws.p, x.st);
+            if (nb) EZ_SHARD_HIP(hipMemcpyAsync(x.r->in.p, in + ib, nb, hipMemcpyHostToDevice, x.r->st));
+            EZ_SHARD_HIP(hipMemcpyAsync(x.r->in_off.p, ioff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.r->st));
+            EZ_SHARD_HIP(hipMemcpyAsync(x.r->out_off.p, ooff.data(), 8 * (c + 1), hipMemcpyHostToDevice, x.r->st));
+            // (the largest slot and the extents given: the decoder route needs no device read-back)
+            ez_batch b{x.r->in.as<uint8_t>(), x.r->in_off.as<uint64_t>(), x.r->out.as<uint8_t>(), x.r->out_off.as<uint64_t>(),
+                       x.r->size.as<uint64_t>(), x.r->status.as<int32_t>(), c, mx ? mx : 1, nb, no};
+            const int r = ez_decompress_batch(block_size_limit, &b, x.r->ws.p, x.r->st);
             if (r != EZ_OK) return r;
-            if (no) EZ_SHARD_HIP(hipMemcpyAsync(out + ob, x.out.p, no, hipMemcpyDeviceToHost, x.st));
-            EZ_SHARD_HIP(hipMemcpyAsync(out_size + x.first, x.size.p, 8 * c, hipMemcpyDeviceToHost, x.st));
-            if (status) EZ_SHARD_HIP(hipMemcpyAsync(status + x.first, x.status.p, 4 * c, hipMemcpyDeviceToHost, x.st));
-            EZ_SHARD_HIP(hipStreamSynchronize(x.st));
+            if (no) EZ_SHARD_HIP(hipMemcpyAsync(out + ob, x.r->out.p, no, hipMemcpyDeviceToHost, x.r->st));
+            EZ_SHARD_HIP(hipMemcpyAsync(out_size + x.first, x.r->size.p, 8 * c, hipMemcpyDeviceToHost, x.r->st));
+            if (status) EZ_SHARD_HIP(hipMemcpyAsync(status + x.first, x.r->status.p, 4 * c, hipMemcpyDeviceToHost, x.r->st));
+            EZ_SHARD_HIP(hipStreamSynchronize(x.r->st));
             return EZ_OK;
         });
     } catch (...) {
         return EZ_EDEVICE;
     }
+}
+
+// Frees the device scratch the batch calls keep between calls (no reference counterpart; like a
+// caching allocator's empty_cache): the K1 / K1c scratch and K2j workspaces per (device, HIP stream),
+// the multi-device calls' pooled shard buffers and the Reader handles' shared K2j workspace, on
+// `device` (< 0: every device).  Scratch a call is using at that moment is kept.
+extern "C" int ez_release_cached(int device) {
+    const int have = device_count();
+    if (have <= 0) return EZ_EDEVICE;
+    if (device >= have) return EZ_EINVAL;
+    DeviceGuard keep(-1);
+    for (int d = device < 0 ? 0 : device; d < (device < 0 ? have : device + 1); d++) {
+        if (hipSetDevice(d) != hipSuccess) return EZ_EDEVICE;
+        k1_cache().trim(d);
+        ez::jump_cache().trim(d);
+        ReaderJws &J = reader_jws(d);
+        if (J.mu.try_lock()) {
+            J.buf.release();
+            J.mu.unlock();
+        }
+    }
+    shard_pool().trim(device);
+    return EZ_OK;
 }

@@ -25,6 +25,7 @@
 // reproduces block[x & mask] exactly:
 //   q = w.pos - bs + ((x - w.pos) mod bs);  byte = q >= start ? p[q-start]
 //                                                  : (ring ? ring[q & mask] : 0)
+#include <atomic>
 #include <string>
 #include <type_traits>
 
@@ -708,14 +709,16 @@ uint64_t compress_scratch_words(const CompressArgs &a) {
 // streams of 64 KiB and more.  EZ_K1=general or ez_select_compress_kernel('w') forces the general
 // kernel alone, 'x' K1x for any fresh single-Write batch with a table of at most 4096 entries
 // (tests, A/B).
-static int g_forced_variant = -1;  // -1: not read yet; 0: automatic; else the kernel's letter
+static std::atomic<int> g_forced_variant{-1};  // -1: not read yet; 0: automatic; else the kernel's letter
 void select_compress_variant(int v) { g_forced_variant = v; }
 
 static int forced_variant() {
-    int &forced = g_forced_variant;
+    int forced = g_forced_variant.load();
     if (forced < 0) {
         const char *e = knob_str("EZ_K1");
-        forced = e && std::string(e) == "general" ? 'w' : (e && std::string(e) == "long" ? 'l' : 0);
+        const int f = e && std::string(e) == "general" ? 'w' : (e && std::string(e) == "long" ? 'l' : 0);
+        (void)g_forced_variant.compare_exchange_strong(forced, f);
+        forced = g_forced_variant.load();
     }
     return forced;
 }

@@ -47,6 +47,8 @@
 
 #include <cstdio>
 #include <cstring>
+#include <atomic>
+#include <mutex>
 #include <type_traits>
 #include <vector>
 
@@ -2727,7 +2729,7 @@ int split_g32(uint64_t count) {
     if (g == 32 || g == 16) return g;
     return count <= 8192 ? 32 : 16;
 }
-bool g_split_t32 = false;  // ez_select_compress_kernel('S')
+std::atomic<bool> g_split_t32{false};  // ez_select_compress_kernel('S')
 bool split_t32_forced() {
     static const bool v = knob("EZ_K1S_T", 0) == 32;
     return v || g_split_t32;
@@ -3081,21 +3083,34 @@ static hipError_t launch_emit_wide(const CompressArgs &a, const uint4 *recs, uin
 // 1,024 x 1 MiB: 115 -> 103 ms); C2's 4,096 streams keep K1L (25 ms against 64 for K1c's passes,
 // which are bound by the parse's instructions there).  EZ_K1C=0 / EZ_K1C_MAXCOUNT (experiment
 // builds) or a forced 'l': K1L alone
+// K1c's workspace is sized by the batch's longest stream (count x kmax chunks of about 400 KB: ~12 x
+// count x max_len); a skewed batch (one long stream among many short ones) would ask for far more than
+// its bytes, so above kK1cMaxBytes the batch takes K1L alone, as it does when the C-ABI cannot
+// allocate it (no_k1c)
+constexpr uint64_t kK1cMaxBytes = (uint64_t)24 << 30;
 bool chunk_applies(const CompressArgs &a) {
     static const bool on = knob("EZ_K1C", 1) != 0;
     static const uint64_t most = (uint64_t)knob("EZ_K1C_MAXCOUNT", 1024);
-    return on && !compress_forced_long() && long_applies(a) && a.count <= most && a.max_len >= 2 * (uint64_t)kc_geom(a).C;
+    return on && !a.no_k1c && !compress_forced_long() && long_applies(a) && a.count <= most &&
+           a.max_len >= 2 * (uint64_t)kc_geom(a).C && kc_layout(a, kc_geom(a)).total <= kK1cMaxBytes;
 }
 
-// verdict counts of K1c batches while counting is on (ez_compress_k1c_stats)
+// verdict counts of K1c batches while counting is on (ez_compress_k1c_stats; the multi-device batches
+// launch from several host threads)
+static std::mutex g_kc_mu;
 static bool g_kc_stats_on = false;
 static uint64_t g_kc_stats[6] = {0, 0, 0, 0, 0, 0};
 void k1c_stats(int enable, uint64_t *out) {
+    std::lock_guard<std::mutex> lk(g_kc_mu);
     if (out)
         for (int t = 0; t < 6; t++) out[t] = g_kc_stats[t];
     if (enable)
         for (int t = 0; t < 6; t++) g_kc_stats[t] = 0;
     g_kc_stats_on = enable != 0;
+}
+static bool kc_stats_on() {
+    std::lock_guard<std::mutex> lk(g_kc_mu);
+    return g_kc_stats_on;
 }
 
 static hipError_t launch_chunk(const CompressArgs &a, uint8_t *recs, hipStream_t st) {
@@ -3143,6 +3158,7 @@ static hipError_t launch_chunk(const CompressArgs &a, uint8_t *recs, hipStream_t
     static const int passes = knob("EZ_K1C_PASSES", 12);
     uint32_t *left = (uint32_t *)(base + l.left);
     static const bool diag = knob("EZ_K1C_DIAG", 0) != 0;
+    const bool stats = kc_stats_on();
     for (int pass = 1; pass <= passes; pass++) {
         if (lw) hipLaunchKernelGGL(kc_parse<true>, dim3(pgrid), dim3(64), lds, st, a, B, pass);
         else hipLaunchKernelGGL(kc_parse<false>, dim3(pgrid), dim3(64), lds, st, a, B, pass);
@@ -3162,7 +3178,7 @@ static hipError_t launch_chunk(const CompressArgs &a, uint8_t *recs, hipStream_t
             stop = h_left == 0;
         }
         const bool final = stop || pass == passes;
-        if (!(diag || (g_kc_stats_on && final))) {
+        if (!(diag || (stats && final))) {
             if (stop) break;
             continue;
         }
@@ -3180,8 +3196,10 @@ static hipError_t launch_chunk(const CompressArgs &a, uint8_t *recs, hipStream_t
             segs += si[kKcInfo * s];
         }
         const uint64_t v[6] = {f[0], f[kKcFailChunk], f[kKcFailSync], f[kKcFailJudge], f[kKcFailCap], segs};
-        if (g_kc_stats_on && final)
+        if (stats && final) {
+            std::lock_guard<std::mutex> lk(g_kc_mu);
             for (int t = 0; t < 6; t++) g_kc_stats[t] += v[t];
+        }
         if (diag)
             fprintf(stderr, "K1c pass %d: %llu streams x %d chunks; proven %llu, chunk %llu, sync %llu, judge %llu, cap %llu; segments %llu\n",
                     pass, (unsigned long long)a.count, g.kmax, (unsigned long long)v[0], (unsigned long long)v[1], (unsigned long long)v[2],

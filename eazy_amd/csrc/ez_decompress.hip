@@ -18,6 +18,8 @@
 
 #include <string.h>
 
+#include <atomic>
+
 namespace ez {
 namespace {
 
@@ -257,9 +259,11 @@ __global__ __launch_bounds__(64) void k2_decompress(DecompressArgs A) {
 // the batch decoders: K2r (lane per stream, slots < 64 KiB) or K2t (token-parallel wave per stream,
 // longer slots), each handing the streams it does not finish to the exact decoder; 'r', 't' / 'w'
 // force one (tests, A/B; K2w is reached only this way)
-static int g_decompress_variant = -1;  // -1: not read yet; 0: automatic; 'r', 't', 'w'
+static std::atomic<int> g_decompress_variant{-1};  // -1: not read yet; 0: automatic; 'r', 't', 'w', 'j'
 void select_decompress_variant(int v) { g_decompress_variant = v; }
-static int g_last_variant = 0;  // the first K2 kernel of the last batch decode ('e': exact alone)
+// the first K2 kernel of the last batch decode ('e': exact alone); atomic: the multi-device batches
+// decode their shards on several host threads
+static std::atomic<int> g_last_variant{0};
 int last_decompress_variant() { return g_last_variant; }
 
 // [slow list: 2 * count + 32 words][K2w / K2t's deferred literals: 4 words + count * kDefSlots records]
@@ -322,17 +326,20 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     hipError_t e = largest_slot(a0, st, &a.max_out);
     if (e != hipSuccess) return e;
     if ((e = hipMemsetAsync(a.slow, 0, sizeof(uint32_t), st)) != hipSuccess) return e;
-    if (g_decompress_variant < 0) {
+    int sel = g_decompress_variant.load();
+    if (sel < 0) {
         const char *v = knob_str("EZ_K2");
-        g_decompress_variant = v && strcmp(v, "wave") == 0 ? 'w'
-                               : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : (v && strcmp(v, "jump") == 0 ? 'j' : 0)));
+        sel = v && strcmp(v, "wave") == 0 ? 'w'
+              : (v && strcmp(v, "ring") == 0 ? 'r' : (v && strcmp(v, "tok") == 0 ? 't' : (v && strcmp(v, "jump") == 0 ? 'j' : 0)));
+        int want = -1;
+        (void)g_decompress_variant.compare_exchange_strong(want, sel);
     }
     const uint64_t exact_grid = a.count < 4096 ? a.count : 4096;
     // Slots under 64 KiB go to K2r's lane per stream; longer ones (C2, C4, the sweep's long streams) to
     // K2t (1 GiB batches, K2 ms, K2r / K2t: 8 KiB 1.89 / 4.99, 16 KiB 1.96 / 4.89, 32 KiB 3.50 / 5.06,
     // 64 KiB 6.69 / 5.31, 128 KiB 13.4 / 5.82, 256 KiB (C2; K2w 12.5) - / 7.0, 1 MiB (K2w 29.7) - / 14.4;
     // C4 fp32 K2w 0.145 / K2t 0.151, C4s 164 / 106 ms).
-    int v = a.force ? a.force : (g_decompress_variant != 0 ? g_decompress_variant : (a.max_out >= long_slot ? 't' : 'r'));
+    int v = a.force ? a.force : (sel != 0 ? sel : (a.max_out >= long_slot ? 't' : 'r'));
     // A few long streams whose output is at least twice their input (copies, not literals) go to
     // K2j: K2t gives each stream one wave and walks its copy chains round by round, K2j the whole
     // chip (C4s, 64 x 4 MiB: K2t 93.7 ms, K2j 11.4 ms; a lone 16 MiB log stream 171 / 11.7 ms).
@@ -340,25 +347,29 @@ hipError_t launch_decompress(const DecompressArgs &a0, hipStream_t st) {
     // batches of more streams, whose chains K2t runs side by side (1,024 x 1 MiB: 12.9 / 58.8 ms).
     // K2j's time follows the batch's output, K2t's the longest stream's (256 x 1 MiB logs: K2t's
     // chain ~12.8 ms against K2j 15.6): K2j only while the output is at most 200 slots' worth.
-    if (v == 't' && !a.force && g_decompress_variant == 0 && a.count <= 256 && a.max_out >= ((uint64_t)1 << 20)) {
-        uint64_t ext[4] = {0, 0, 0, 0};  // (the offsets may be a view into a larger batch's: absolute)
-        if ((e = hipMemcpyAsync(&ext[0], a.in_off, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-        if ((e = hipMemcpyAsync(&ext[1], a.in_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-        if ((e = hipMemcpyAsync(&ext[2], a.out_off, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-        if ((e = hipMemcpyAsync(&ext[3], a.out_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        const uint64_t nin = ext[1] - ext[0], nout = ext[3] - ext[2];
+    // The extents are the caller's hints (ez_batch.in_bytes / out_bytes); without them, four offsets
+    // read back (which waits for the stream).
+    if (v == 't' && !a.force && sel == 0 && a.count <= 256 && a.max_out >= ((uint64_t)1 << 20)) {
+        uint64_t nin = 0, nout = 0;
+        if ((e = batch_extents(a, st, &nin, &nout)) != hipSuccess) return e;
+        a.in_bytes = nin;
+        a.out_bytes = nout;
         if (nin >= (uint64_t)a.count * (64 << 10) && nout >= 2 * nin && nout <= 200 * a.max_out) v = 'j';
     }
     if (v == 'j' && !jump_applies(a)) v = 't';
-    g_last_variant = v;
     if (v == 'j') {
-        // K2j: few long streams with the whole chip; its hand-overs go to the exact decoder
+        // K2j: few long streams with the whole chip; its hand-overs go to the exact decoder.  Without
+        // its workspace (a failed allocation, nothing launched) the batch takes K2t.
         e = launch_decompress_jump(a, st);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k2_decompress, dim3((unsigned)exact_grid), dim3(64), 0, st, a);
-        return hipGetLastError();
+        if (e == hipSuccess) {
+            g_last_variant = v;
+            hipLaunchKernelGGL(k2_decompress, dim3((unsigned)exact_grid), dim3(64), 0, st, a);
+            return hipGetLastError();
+        }
+        if (e != hipErrorOutOfMemory) return e;
+        v = 't';
     }
+    g_last_variant = v;
     if (v == 't') {
         // K2t: token-parallel, a wave per stream; its hand-overs go to the exact decoder, the long
         // literals it defers are moved last (the exact decoder writes the same bytes for a stream it takes)

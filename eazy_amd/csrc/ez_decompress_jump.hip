@@ -37,10 +37,8 @@
 // a slot too small) go to the exact decoder (ez_decompress.hip), which recomputes them from the start.
 #include <hip/hip_runtime.h>
 
-#include <map>
-#include <mutex>
-
 #include "ez_bytes.h"
+#include "ez_cache.h"
 #include "ez_internal.h"
 #include "ez_k2_parse.h"
 
@@ -121,7 +119,8 @@ __global__ __launch_bounds__(1024) void kj_init(DecompressArgs A, JWork W) {
             const uint64_t cap = A.out_off[s + 1] - A.out_off[s];
             nch = nb == 0 ? 1u : (uint32_t)((nb + kJC - 1) / kJC);
             JHead h{};
-            h.state = (nb >= (1ull << 31) || cap >= (1ull << 32) - 2 || A.out_off[s + 1] >= (1ull << 32) - 2) ? 1u : 0u;
+            // (pointers are 32-bit offsets from the batch's first output slot, rounded down to 16 bytes)
+            h.state = (nb >= (1ull << 31) || cap >= (1ull << 32) - 2 || A.out_off[s + 1] - (A.out_off[0] & ~15ull) >= (1ull << 32) - 2) ? 1u : 0u;
             h.bsl = -1;
             h.nchunk = nch;
             W.head[s] = h;
@@ -363,9 +362,11 @@ __global__ __launch_bounds__(64) void kj_emit(DecompressArgs A, JWork W) {
 }
 
 // ---- 3: literal and zero bytes, and a pointer for every copied byte (thread per 16 output bytes)
-// output bytes [q, q + n) of stream s (n <= 16, inside its output): bytes into by, pointers into pt
+// output bytes [q, q + n) of stream s (n <= 16, inside its output): bytes into by, pointers into pt.
+// Pointers and the ptr array count from g0 = out_off[0] rounded down to 16 bytes: a batch may be a view
+// into a larger one (absolute offsets), whose bytes before out_off[0] are never touched.
 __device__ __forceinline__ void kj_piece(const DecompressArgs &A, const JWork &W, const JHead &H, uint32_t s, uint64_t q, uint32_t n,
-                                         uint32_t *by, uint32_t *pt) {
+                                         uint64_t g0, uint32_t *by, uint32_t *pt) {
     const uint64_t base = A.out_off[s];
     const uint32_t p0 = (uint32_t)(q - base);
     // the token holding p0: the last record with dst <= p0; the next ones by walking on
@@ -380,7 +381,7 @@ __device__ __forceinline__ void kj_piece(const DecompressArgs &A, const JWork &W
     uint32_t nxt = a + 1 < H.ntok ? tk[a + 1].dst : 0xffffffffu;
     const uint8_t *in = A.in + A.in_off[s];
     if (n == 16 && p0 + 16 <= t.dst + t.L) {  // the 16 bytes inside one token (long literals, runs, zeros)
-        const uint32_t x = (uint32_t)(base + p0);
+        const uint32_t x = (uint32_t)(base + p0 - g0);
         if (t.kd == 0) {
             const uint8_t *y = in + t.src + (p0 - t.dst);
             const V16 v = y + 16 <= A.in + A.in_off[A.count] ? ld16v(y) : ld_clamped(y, A.in, A.in + A.in_off[A.count]);
@@ -401,7 +402,7 @@ __device__ __forceinline__ void kj_piece(const DecompressArgs &A, const JWork &W
             t = tk[a];
             nxt = a + 1 < H.ntok ? tk[a + 1].dst : 0xffffffffu;
         }
-        const uint32_t x = (uint32_t)(base + p);
+        const uint32_t x = (uint32_t)(base + p - g0);
         uint32_t v = 0;
         if (t.kd == 0) {  // literal
             v = in[t.src + (p - t.dst)];
@@ -417,38 +418,41 @@ __device__ __forceinline__ void kj_piece(const DecompressArgs &A, const JWork &W
 }
 
 __global__ __launch_bounds__(256) void kj_expand(DecompressArgs A, JWork W) {
-    const uint64_t end = A.out_off[A.count];
-    for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; g < end; g += (uint64_t)gridDim.x * blockDim.x * 16) {
-        // the stream of the piece's first byte (binary search over the slots)
+    const uint64_t ob = A.out_off[0], g0 = ob & ~15ull, end = A.out_off[A.count];
+    for (uint64_t g = g0 + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; g < end; g += (uint64_t)gridDim.x * blockDim.x * 16) {
+        // the stream of the piece's first byte of the batch (binary search over the slots)
+        const uint64_t x0 = g > ob ? g : ob;
         uint32_t s = 0, hs = (uint32_t)A.count;
         while (hs - s > 1) {
             const uint32_t m = (s + hs) >> 1;
-            if (A.out_off[m] <= g) s = m;
+            if (A.out_off[m] <= x0) s = m;
             else hs = m;
         }
         const uint64_t ge = g + 16 < end ? g + 16 : end;
         const JHead H = W.head[s];
-        if (!H.state && A.out_off[s] + H.total >= g + 16 && ge == g + 16) {
+        if (!H.state && A.out_off[s] <= g && A.out_off[s] + H.total >= g + 16 && ge == g + 16) {
             // the common case: the 16 bytes all in stream s's output, one store of each kind
             uint32_t by[4] = {0, 0, 0, 0}, pt[16];
-            kj_piece(A, W, H, s, g, 16, by, pt);
+            kj_piece(A, W, H, s, g, 16, g0, by, pt);
             *(uint4 *)(A.out + g) = make_uint4(by[0], by[1], by[2], by[3]);  // (copied bytes: kj_gather)
+            uint32_t *pp = W.ptr + (g - g0);
 #pragma unroll
-            for (int q = 0; q < 4; q++) *(uint4 *)(W.ptr + g + 4 * q) = make_uint4(pt[4 * q], pt[4 * q + 1], pt[4 * q + 2], pt[4 * q + 3]);
+            for (int q = 0; q < 4; q++) *(uint4 *)(pp + 4 * q) = make_uint4(pt[4 * q], pt[4 * q + 1], pt[4 * q + 2], pt[4 * q + 3]);
             continue;
         }
-        // a piece at a slot's end: each stream's output bytes in it, byte by byte
-        for (uint64_t x = g; x < ge;) {
+        // a piece at a slot's end (or before the batch's first slot): each stream's output bytes in it,
+        // byte by byte
+        for (uint64_t x = x0; x < ge;) {
             while (s + 1 < (uint32_t)A.count && A.out_off[s + 1] <= x) s++;
             const JHead Hs = W.head[s];
-            const uint64_t ob = A.out_off[s] + Hs.total, se = A.out_off[s + 1] < ge ? A.out_off[s + 1] : ge;
-            if (!Hs.state && x < ob) {
-                const uint32_t n = (uint32_t)((ob < se ? ob : se) - x);
+            const uint64_t ob2 = A.out_off[s] + Hs.total, se = A.out_off[s + 1] < ge ? A.out_off[s + 1] : ge;
+            if (!Hs.state && x < ob2) {
+                const uint32_t n = (uint32_t)((ob2 < se ? ob2 : se) - x);
                 uint32_t by[4] = {0, 0, 0, 0}, pt[16];
-                kj_piece(A, W, Hs, s, x, n, by, pt);
+                kj_piece(A, W, Hs, s, x, n, g0, by, pt);
                 for (uint32_t k = 0; k < n; k++) {
                     A.out[x + k] = (uint8_t)(by[k >> 2] >> (8 * (k & 3)));
-                    W.ptr[x + k] = pt[k];
+                    W.ptr[x - g0 + k] = pt[k];
                 }
             }
             x = se;
@@ -459,7 +463,7 @@ __global__ __launch_bounds__(256) void kj_expand(DecompressArgs A, JWork W) {
 // ---- 4: one pointer-jumping pass (returns at once when the pass before changed nothing)
 __global__ __launch_bounds__(256) void kj_jump(DecompressArgs A, JWork W, int pass) {
     if (pass > 0 && W.pass[pass - 1] == 0) return;
-    const uint64_t end = A.out_off[A.count];
+    const uint64_t end = A.out_off[A.count] - (A.out_off[0] & ~15ull);  // (ptr counts from g0)
     bool changed = false;
     for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; g < end; g += (uint64_t)gridDim.x * blockDim.x * 4) {
         uint4 v = g + 4 <= end ? *(const uint4 *)(W.ptr + g) : make_uint4(kJGap, kJGap, kJGap, kJGap);
@@ -489,12 +493,13 @@ __global__ __launch_bounds__(256) void kj_jump(DecompressArgs A, JWork W, int pa
 
 // ---- 5a: every copied byte from its resolved source
 __global__ __launch_bounds__(256) void kj_gather(DecompressArgs A, JWork W) {
-    const uint64_t end = A.out_off[A.count];
+    const uint64_t g0 = A.out_off[0] & ~15ull, end = A.out_off[A.count] - g0;
+    uint8_t *o = A.out + g0;
     for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; g < end; g += (uint64_t)gridDim.x * blockDim.x * 4) {
         for (uint64_t x = g; x < g + 4 && x < end; x++) {
             const uint32_t q = W.ptr[x];
             if (q == kJGap || q == (uint32_t)x) continue;
-            A.out[x] = q == kJZero ? (uint8_t)0 : A.out[q];
+            o[x] = q == kJZero ? (uint8_t)0 : o[q];
         }
     }
 }
@@ -516,14 +521,6 @@ __global__ __launch_bounds__(256) void kj_final(DecompressArgs A, JWork W) {
         }
     }
 }
-
-// the workspace of a (device, HIP stream), grown as batches need (one launch sequence at a time)
-struct JScratch {
-    void *p = nullptr;
-    size_t cap = 0;
-};
-std::mutex g_jmu;
-std::map<std::pair<int, hipStream_t>, JScratch> g_jws;
 
 size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
@@ -549,6 +546,12 @@ struct JLayout {
 };
 }  // namespace
 
+// K2j's workspaces per (device, HIP stream) (ez_cache.h)
+DevCache &jump_cache() {
+    static DevCache *c = new DevCache();  // (never destroyed: no hipFree after the runtime's teardown)
+    return *c;
+}
+
 // Streams K2j takes: a batch of at most 1,024 streams (slots below 4 GiB in all)
 bool jump_applies(const DecompressArgs &a) { return a.count >= 1 && a.count <= 1024; }
 
@@ -556,36 +559,46 @@ uint64_t jump_workspace_bytes(uint64_t count, uint64_t in_total, uint64_t out_to
     return JLayout(count, in_total, out_total).total;
 }
 
-hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
-    // the batch's input and output extents (one read back: the workspace is sized from them)
-    uint64_t ext[2] = {0, 0};
+hipError_t batch_extents(const DecompressArgs &a, hipStream_t st, uint64_t *in_bytes, uint64_t *out_bytes) {
+    if (a.in_bytes || a.out_bytes) {
+        *in_bytes = a.in_bytes;
+        *out_bytes = a.out_bytes;
+        return hipSuccess;
+    }
+    uint64_t ext[4] = {0, 0, 0, 0};  // (the offsets may be a view into a larger batch's: absolute)
     hipError_t e;
-    if ((e = hipMemcpyAsync(&ext[0], a.in_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
-    if ((e = hipMemcpyAsync(&ext[1], a.out_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&ext[0], a.in_off, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&ext[1], a.in_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&ext[2], a.out_off, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
+    if ((e = hipMemcpyAsync(&ext[3], a.out_off + a.count, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) return e;
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    const uint64_t in_total = ext[0], out_total = ext[1];
+    *in_bytes = ext[1] - ext[0];
+    *out_bytes = ext[3] - ext[2];
+    return hipSuccess;
+}
+
+hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
+    // the batch's input and output extents (the caller's hints, else one read back): the workspace is
+    // sized from them; the ptr array covers out_off[0] rounded down to 16 bytes .. out_off[count]
+    uint64_t in_total = 0, out_bytes = 0;
+    hipError_t e = batch_extents(a, st, &in_total, &out_bytes);
+    if (e != hipSuccess) return e;
+    const uint64_t out_total = out_bytes + 16;
     const JLayout Y(a.count, in_total, out_total);
     const uint64_t chunks = Y.chunks, tok_cap = Y.tok_cap;
     const size_t o_head = Y.o_head, o_cbase = Y.o_cbase, o_entry = Y.o_entry, o_sexit = Y.o_sexit, o_bits = Y.o_bits, o_cnt = Y.o_cnt,
                  o_cout = Y.o_cout, o_cflag = Y.o_cflag, o_ctb = Y.o_ctb, o_cob = Y.o_cob, o_tok = Y.o_tok, o_ptr = Y.o_ptr,
                  o_pass = Y.o_pass;
-    // the caller's workspace when it gives one large enough, else this (device, stream)'s (the lock
+    // the caller's workspace when it gives one large enough, else this (device, stream)'s (its lease
     // is held through the launches: another host thread growing it meanwhile would free it under them)
-    std::unique_lock<std::mutex> lk(g_jmu, std::defer_lock);
+    CacheLease lease;
     uint8_t *w = (uint8_t *)a.jws;
     if (!w || a.jws_cap < Y.total) {
         int dev = 0;
         if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
-        lk.lock();
-        JScratch &sc = g_jws[std::make_pair(dev, st)];
-        if (sc.cap < Y.total) {
-            if (sc.p) (void)hipFree(sc.p);
-            sc.p = nullptr;
-            sc.cap = 0;
-            if ((e = hipMalloc(&sc.p, Y.total + Y.total / 4)) != hipSuccess) return e;
-            sc.cap = Y.total + Y.total / 4;
-        }
-        w = (uint8_t *)sc.p;
+        lease = jump_cache().acquire(dev, (void *)st);
+        if (!lease->ensure(Y.total)) return hipErrorOutOfMemory;  // (the caller decodes the batch on K2t)
+        w = (uint8_t *)lease->p;
     }
     JWork W{};
     W.head = (JHead *)(w + o_head);
@@ -612,7 +625,7 @@ hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(kj_count, dim3(cgrid), dim3(64), 0, st, a, W);
     hipLaunchKernelGGL(kj_scan, dim3((unsigned)a.count), dim3(64), 0, st, a, W, tok_alloc);
     hipLaunchKernelGGL(kj_emit, dim3(cgrid), dim3(64), 0, st, a, W);
-    const uint64_t pieces = (out_total + 15) / 16;
+    const uint64_t pieces = (out_total + 15) / 16;  // (out_total: the batch's output and the alignment slack)
     const unsigned egrid = (unsigned)(pieces / 256 + 1 < 8192 ? pieces / 256 + 1 : 8192);
     hipLaunchKernelGGL(kj_expand, dim3(egrid), dim3(256), 0, st, a, W);
     const uint64_t quads = (out_total + 3) / 4;

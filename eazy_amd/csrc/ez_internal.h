@@ -72,6 +72,7 @@ struct CompressArgs {
     SpecLit *spec_lit;
     uint32_t *spec_nlit;
     uint32_t win_bytes;       // general kernel, long streams: LDS window bytes (set by its launcher)
+    int no_k1c;               // K1c's workspace could not be had: K1L alone (set by the C-ABI's retry)
 };
 
 
@@ -123,6 +124,9 @@ struct DecompressArgs {
     void *jws;
     uint64_t jws_cap;
     int force;                // batch: the first K2 kernel ('r', 't', ...; 0 = the automatic / selected one)
+    // batch: host hints, in_off[count] - in_off[0] and out_off[count] - out_off[0] (0 = unknown: the
+    // K2j route and its workspace then read the offsets back, which waits for the stream)
+    uint64_t in_bytes, out_bytes;
 };
 
 // words of workspace the two-level batch decoder needs
@@ -170,7 +174,12 @@ hipError_t launch_defer_copy(const DecompressArgs &a, hipStream_t s);       // K
 // records and pointer jumping over the copied bytes; streams it cannot take go to slow
 bool jump_applies(const DecompressArgs &a);
 uint64_t jump_workspace_bytes(uint64_t count, uint64_t in_total, uint64_t out_total);
+// (hipErrorOutOfMemory: its workspace could not be had, nothing was launched)
 hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t s);
+class DevCache;
+DevCache &jump_cache();  // K2j's workspaces per (device, HIP stream)
+// in_off[count] - in_off[0], out_off[count] - out_off[0]: the caller's hints, else read back (waits)
+hipError_t batch_extents(const DecompressArgs &a, hipStream_t s, uint64_t *in_bytes, uint64_t *out_bytes);
 hipError_t launch_decompress_tok(const DecompressArgs &a, hipStream_t s);   // K2t, token-parallel wave per stream
 bool lds_exchange_in_lane_order();  // the LDS property K1s-T32 relies on (checked once)
 bool lds_mskor_in_lane_order();     // the LDS property k1_lean's one-atomic visit relies on (checked once)

@@ -115,6 +115,14 @@ func compressStreams(streams [][][]byte, block, htable int) ([][]byte, error) {
 			}
 		}
 	}()
+	// every HIP call's result is checked: a failed copy must never hand back stale bytes as success
+	// (the errors surface as the reference's do, writer.go:387-401)
+	hip := func(r C.hipError_t) error {
+		if r != C.hipSuccess {
+			return ErrDevice
+		}
+		return nil
+	}
 	for _, a := range []struct {
 		p *unsafe.Pointer
 		n uint64
@@ -126,19 +134,29 @@ func compressStreams(streams [][][]byte, block, htable int) ([][]byte, error) {
 		}
 	}
 	if len(host) > 0 {
-		C.hipMemcpy(dIn, unsafe.Pointer(&host[0]), C.size_t(len(host)), C.hipMemcpyHostToDevice)
+		if err := hip(C.hipMemcpy(dIn, unsafe.Pointer(&host[0]), C.size_t(len(host)), C.hipMemcpyHostToDevice)); err != nil {
+			return nil, err
+		}
 	}
-	C.hipMemcpy(dInOff, unsafe.Pointer(&inOff[0]), C.size_t(8*(count+1)), C.hipMemcpyHostToDevice)
-	C.hipMemcpy(dOutOff, unsafe.Pointer(&outOff[0]), C.size_t(8*(count+1)), C.hipMemcpyHostToDevice)
+	if err := hip(C.hipMemcpy(dInOff, unsafe.Pointer(&inOff[0]), C.size_t(8*(count+1)), C.hipMemcpyHostToDevice)); err != nil {
+		return nil, err
+	}
+	if err := hip(C.hipMemcpy(dOutOff, unsafe.Pointer(&outOff[0]), C.size_t(8*(count+1)), C.hipMemcpyHostToDevice)); err != nil {
+		return nil, err
+	}
 	b := C.ez_batch{
 		in: (*C.uint8_t)(dIn), in_off: (*C.uint64_t)(dInOff), out: (*C.uint8_t)(dOut), out_off: (*C.uint64_t)(dOutOff),
 		out_size: (*C.uint64_t)(dSize), status: (*C.int32_t)(dStatus), count: C.uint64_t(count), max_len: C.uint64_t(maxLen),
 	}
 	var st C.int
 	if multi {
-		C.hipMemcpy(dWIdx, unsafe.Pointer(&writeIdx[0]), C.size_t(8*(count+1)), C.hipMemcpyHostToDevice)
+		if err := hip(C.hipMemcpy(dWIdx, unsafe.Pointer(&writeIdx[0]), C.size_t(8*(count+1)), C.hipMemcpyHostToDevice)); err != nil {
+			return nil, err
+		}
 		if len(writeEnd) > 0 {
-			C.hipMemcpy(dWEnd, unsafe.Pointer(&writeEnd[0]), C.size_t(8*len(writeEnd)), C.hipMemcpyHostToDevice)
+			if err := hip(C.hipMemcpy(dWEnd, unsafe.Pointer(&writeEnd[0]), C.size_t(8*len(writeEnd)), C.hipMemcpyHostToDevice)); err != nil {
+				return nil, err
+			}
 		}
 		st = C.ez_compress_batch_writes(C.int64_t(block), C.int64_t(htable), 0, &b, (*C.uint64_t)(dWIdx),
 			(*C.uint64_t)(dWEnd), C.uint64_t(maxWrites), nil)
@@ -151,9 +169,16 @@ func compressStreams(streams [][][]byte, block, htable int) ([][]byte, error) {
 	out := make([]byte, outOff[count])
 	size := make([]uint64, count)
 	status := make([]int32, count)
-	C.hipMemcpy(unsafe.Pointer(&out[0]), dOut, C.size_t(len(out)), C.hipMemcpyDeviceToHost)
-	C.hipMemcpy(unsafe.Pointer(&size[0]), dSize, C.size_t(8*count), C.hipMemcpyDeviceToHost)
-	C.hipMemcpy(unsafe.Pointer(&status[0]), dStatus, C.size_t(4*count), C.hipMemcpyDeviceToHost)
+	// (hipMemcpy to host waits for the batch's kernels on the null stream, and reports their faults)
+	if err := hip(C.hipMemcpy(unsafe.Pointer(&out[0]), dOut, C.size_t(len(out)), C.hipMemcpyDeviceToHost)); err != nil {
+		return nil, err
+	}
+	if err := hip(C.hipMemcpy(unsafe.Pointer(&size[0]), dSize, C.size_t(8*count), C.hipMemcpyDeviceToHost)); err != nil {
+		return nil, err
+	}
+	if err := hip(C.hipMemcpy(unsafe.Pointer(&status[0]), dStatus, C.size_t(4*count), C.hipMemcpyDeviceToHost)); err != nil {
+		return nil, err
+	}
 	res := make([][]byte, count)
 	for k := range streams {
 		if status[k] != 0 {

@@ -21,7 +21,7 @@
 extern "C" {
 #endif
 
-#define EZ_ABI_VERSION 1
+#define EZ_ABI_VERSION 2
 
 /* ---- status codes: one per reference error value (reader.go:57-76) ---- */
 enum {
@@ -173,7 +173,12 @@ typedef struct {
     uint64_t *out_size;      /* count: bytes written into each slot */
     int32_t *status;         /* count: EZ_* per stream (may be NULL) */
     uint64_t count;
-    uint64_t max_len;        /* host hint: max input length of a stream (0 = unknown) */
+    uint64_t max_len;        /* host hint: max input length of a stream (decompress: max slot; 0 = unknown) */
+    /* decompress, host hints (ABI 2): in_off[count] - in_off[0] and out_off[count] - out_off[0],
+     * both 0 = unknown.  With them the decoder route and its workspace need no read-back of the
+     * offsets, so the call never waits for the stream; compress ignores them. */
+    uint64_t in_bytes;
+    uint64_t out_bytes;
 } ez_batch;
 
 #define EZ_F_NO_MAGIC 0x1 /* compress: AppendMagic = false */
@@ -226,6 +231,17 @@ int ez_compress_batch_multi(int64_t block, int64_t htable, int flags, const uint
 int ez_decompress_batch_multi(int64_t block_size_limit, const uint8_t *in, const uint64_t *in_off, uint64_t count,
                               const int *devices, int ndev, uint8_t *out, const uint64_t *out_off, uint64_t *out_size,
                               int32_t *status);
+
+/* Frees the device scratch kept between batch calls (no reference counterpart; a caching
+ * allocator's empty_cache): K1 / K1c scratch and K2j workspaces per (device, HIP stream), the
+ * multi-device calls' pooled shard buffers, the Reader handles' shared K2j workspace; device < 0 =
+ * every device.  Scratch in use by a concurrent call is kept.  Entries beyond 8 streams per device
+ * are also freed least recently used first as new streams arrive. */
+int ez_release_cached(int device);
+/* Introspection (tests, measurement): the shards of the last ez_*_batch_multi call in this process
+ * (returns their number; up to cap entries filled, any pointer may be NULL): each shard's device and
+ * its device interval (upload to download) in ms from the earliest shard start on that device. */
+int ez_multi_last_shards(int *dev, double *t0_ms, double *t1_ms, int cap);
 
 /* Introspection (no reference counterpart): the K1 kernel a batch of `count`
  * fresh streams of <= max_len bytes would run on the current device, as a
