@@ -635,9 +635,22 @@ struct WinLds {
         w1.lo = (uint64_t)b[4] | ((uint64_t)b[5] << 32);
         w1.hi = (uint64_t)b[6] | ((uint64_t)b[7] << 32);
     }
-    // x-8 .. x+39 (R = 64: o <= 79, the reads end at byte 131 of the 144-byte buffer)
+    // x-8 .. x+39 (R = 64: o <= 79, the reads end at byte 131 of the 144-byte buffer).  (EZ_EXP &
+    // 131072 builds: three byte-addressed ds_read_b128 -- the LDS runs in unaligned mode under ROCm --
+    // which save 14 VALU per window, the 12 v_alignbyte among them, but measured slower: C1 K1 2.13
+    // against 1.96 ms, two alternating runs on one box; the unaligned reads cost the LDS more cycles)
     __device__ __forceinline__ void bytes48(int32_t i, int g, int lj, V16 &w0, V16 &w1, V16 &w2) const {
         static_assert(R <= 64, "48-byte windows need the region to reach i + 54");
+#if (EZ_EXP & 131072)
+        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+        typedef u32x4 __attribute__((aligned(1))) u32x4u;
+        const uint8_t *u = wl + (uint32_t)(i - 8 - cb + lj);
+        const u32x4 ua = *(const u32x4u *)u, ub = *(const u32x4u *)(u + 16), uc = *(const u32x4u *)(u + 32);
+        w0 = V16{(uint64_t)ua.x | ((uint64_t)ua.y << 32), (uint64_t)ua.z | ((uint64_t)ua.w << 32)};
+        w1 = V16{(uint64_t)ub.x | ((uint64_t)ub.y << 32), (uint64_t)ub.z | ((uint64_t)ub.w << 32)};
+        w2 = V16{(uint64_t)uc.x | ((uint64_t)uc.y << 32), (uint64_t)uc.z | ((uint64_t)uc.w << 32)};
+        return;
+#endif
         const uint32_t o = (uint32_t)(i - 8 - cb + lj), r = o & 3;
         const uint32_t *q = (const uint32_t *)(wl + (o & ~3u));
         uint32_t d[13];
@@ -700,9 +713,10 @@ __device__ __forceinline__ void bytes32(const LeanIn &L, const uint8_t *p, int32
 // y-8 .. y+39 (the 40-byte judgement): dwordx4 x3 + dword from floor4(p + y - 8), unchecked (padded
 // streams: k1_lean's edge slots leave 64 readable bytes after every stream)
 __device__ __forceinline__ void bytes48(const LeanIn &L, const uint8_t *p, int32_t y, V16 &c0, V16 &c1, V16 &c2) {
-    const uintptr_t a = (uintptr_t)(p + y - 8);
+    // (floor4(p + y - 8) = floor4(p + y) - 8: one address add, the -8 in the loads' offsets)
+    const uintptr_t a = (uintptr_t)(p + y);
     const uint32_t r = (uint32_t)(a & 3);
-    const uint8_t *w = (const uint8_t *)(a & ~(uintptr_t)3);
+    const uint8_t *w = (const uint8_t *)(a & ~(uintptr_t)3) - 8;
     const uint4 q0 = L.dw4(w), q1 = L.dw4(w + 16), q2 = L.dw4(w + 32);
     const uint32_t q3 = L.dw(w + 48);
     const uint32_t d[13] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w, q2.x, q2.y, q2.z, q2.w, q3};
@@ -905,7 +919,7 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
     V16 w0{0, 0}, w1{0, 0}, w2{0, 0};  // bytes x-8 .. x+7, x+8 .. x+23 (and x+24 .. x+39) of this lane's x
     for (;;) {
         // groups whose stream ended: its size word, then (PERSIST) the next stream
-        if (__ballot(!live && pending) != 0) {
+        if (__builtin_amdgcn_ballot_w64(!live && pending) != 0) {
             if (!live && pending) {
                 if (lj == 0) A.out_size[s] = (uint64_t)((EZ_EXP & 32768) ? 0 : nrec) | ((uint64_t)err << 48);
                 pending = false;
@@ -916,10 +930,10 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
                     open();
                 }
             }
-            if (PERSIST) budget += (int64_t)(4 * A.max_len + 64) * (__builtin_popcountll(__ballot(pending)) / G);
+            if (PERSIST) budget += (int64_t)(4 * A.max_len + 64) * (__builtin_popcountll(__builtin_amdgcn_ballot_w64(pending)) / G);
         }
-        if (__ballot(live) == 0) {
-            if (PERSIST && __ballot(pending) != 0) continue;
+        if (__builtin_amdgcn_ballot_w64(live) == 0) {
+            if (PERSIST && __builtin_amdgcn_ballot_w64(pending) != 0) continue;
             break;
         }
         if (budget < 0) {
@@ -928,7 +942,7 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
             continue;
         }
         // the parse, until one of the groups' streams ends (the bookkeeping above stays out of it)
-        const uint64_t lm = __ballot(live);
+        const uint64_t lm = __builtin_amdgcn_ballot_w64(live);
         do {
         budget--;
         if constexpr (W40) wr.bytes48(i, g, lj, w0, w1, w2);
@@ -995,7 +1009,7 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
             ext = (jf == CAP && (rl ? n - x : (done - cand < n - x ? done - cand : n - x)) > CAP ? 1 : 0) |
                   (jb == 8 && bl > 8 ? 2 : 0);
         }
-        const uint64_t am64 = __ballot(acc);
+        const uint64_t am64 = __builtin_amdgcn_ballot_w64(acc);
         const uint32_t am = (uint32_t)(am64 >> (G * g)) & kGMask;
         const int a = am ? __builtin_ctz(am) : -1;
 #if (EZ_EXP & 65536)
@@ -1009,7 +1023,7 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
         // (one ds_bpermute from each group's first acceptor: fewer VALU than four v_readlane + selects)
         const int32_t sel = __builtin_amdgcn_ds_bpermute(4 * (G * g + (a < 0 ? 0 : a)), pack);
         int32_t nxt = sel & 0x0fffffff;
-        if (__ballot(act && ((sel >> 28) & 3) != 0) != 0) {
+        if (__builtin_amdgcn_ballot_w64(act && ((sel >> 28) & 3) != 0) != 0) {
             // rare: a saturated count; exact lengths by the whole group (as k1_parse)
             // the acceptor's candidate, capped backward count (<= 8) and branch
             const int32_t info = cand | (((zr ? cand : x) - lit) << 16) | ((int32_t)rl << 29) | ((int32_t)zr << 30);
@@ -1078,7 +1092,7 @@ __device__ __forceinline__ void lean_run(const CompressArgs &A, int lj, int g, u
             __builtin_nontemporal_store(rv, rec + (uint32_t)(nrec & 1));
 #endif
         }
-        } while (__ballot(live) == lm && budget >= 0);
+        } while (__builtin_amdgcn_ballot_w64(live) == lm && budget >= 0);
     }
 }
 

@@ -37,7 +37,9 @@ constexpr int32_t kRingStride = 16 + kRing + 16 + 16;
 constexpr int32_t kNear = kRing - 16;    // copies this close read the ring
 constexpr int kRingBlock = 256;          // lanes per block (one wave per SIMD of a CU)
 constexpr int32_t kChunk = 128;          // output leaves the ring in whole 128-byte lines
-constexpr uint32_t kMaxFlushPer = 16;    // kChunk + 16 * (16 + 1) < kRing
+// a step moves <= 16 bytes, plus a paired short literal's <= 15 (below): the unflushed output stays
+// below kChunk + 31 * (fper + 1) + 16 <= kRing for fper <= 8
+constexpr uint32_t kMaxFlushPer = 8;
 
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 
@@ -96,6 +98,10 @@ __host__ __device__ __forceinline__ V16 win16(V16 a, V16 b, uint32_t o) {
     const uint64_t w2 = q == 0 ? b.lo : b.hi;  // (q == 2: o == 16, r == 0: w2 unused)
     return V16{fun8(w0, w1, r), fun8(w1, w2, r)};
 }
+
+#ifndef __HIP_DEVICE_COMPILE__
+inline uint64_t g_ring_iters = 0;
+#endif
 
 // decodes stream s with `ring` (kRing + 16 bytes, with 16-byte guards on both sides) as its history; false = hand
 // the stream over (host-compilable: tools/ring_emu.hip runs it on the CPU)
@@ -204,6 +210,34 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         np = np && !ho;
         const int32_t i0 = i;
         i = np ? i + adv : i;
+        // ---- a short literal and the copy after it in one step (!HW): the literal's
+        // bytes are in the header already (src 1), so when the copy's header lies in the same 16
+        // bytes the literal is stored right after this step's move and the copy becomes the lane's
+        // next token -- one iteration per literal-copy pair instead of two (C1's logs: 462 -> ~343
+        // iterations per stream)
+        bool pair = false;
+        int32_t L1 = 0;
+#if (EZ_EXP & (1 << 27))  // (timing builds: one token per step, A/B)
+        if (false) {
+#else
+        if (!HW) {
+#endif
+            const uint32_t o2 = 1u + (uint32_t)L;  // (the fast path's 1-byte tag; o2 <= 11 below)
+            const uint64_t h2 = o2 < 8 ? (h.lo >> (8 * o2)) | (h.hi << (64 - 8 * o2)) : h.hi >> (8 * (o2 & 7));
+            int32_t L2, adv2;
+            uint32_t D2;
+            bool cp2;
+            const int32_t ft2 = fast_tok(h2, L2, adv2, D2, cp2);
+            pair = np && f && !cp && cp2 && o2 <= 11 &&
+                   (ft2 | (16 - (int32_t)o2 - adv2) | (nb - i - adv2) | (cap - pos - L - L2) | (lim32 - L2) | (win - (int32_t)D2)) >= 0;
+            if (pair) {
+                L1 = L;
+                L = L2;
+                D = D2;
+                cp = true;
+                i += adv2;
+            }
+        }
         // the next header (lanes not parsing reload theirs), one load for every lane: near the
         // batch's end from its last 16 bytes, shifted after the wait at the next iteration's top
         if (HW) {
@@ -241,6 +275,9 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         so += kk;
         rp += kk;
         rem -= kk;
+        if (pair) ring_st(ring, dst, hv);  // the paired literal at the output position (dst == pos)
+        dst = pair ? dst + L1 : dst;
+        pos = pair ? pos + L1 : pos;
         // ---- the next token's state (a padding or meta step has L = 0: no move)
         const bool run = cp && D < 16;
         rem = np ? L : rem;
@@ -263,7 +300,7 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         // one nearly every iteration for the few lanes that just finished a chunk (16-byte
         // pieces stored every iteration, and the fixed store count that lets the waits count
         // past them, measured slower: 0.75 against 0.57 ms at C1)
-        // (unflushed output stays below kChunk + 16 * (fper + 1) <= kRing bytes)
+        // (unflushed output stays below kChunk + 31 * (fper + 1) <= kRing - 16 bytes)
         if ((++it & (fper - 1)) == 0) {
 #if (EZ_EXP & (1 << 26))  // timing builds: no flush (wrong bytes)
             if (it) {} else
@@ -297,6 +334,9 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
             sched_fence();            // (issued here, not sunk to the next iteration's parse)
         }
     }
+#ifndef __HIP_DEVICE_COMPILE__
+    g_ring_iters += it;  // (the host emulation counts the iterations: tools/ring_emu)
+#endif
     if (!slow) {  // the last partial chunk, exact bytes
         int32_t q = fl;
         for (; q + 16 <= pos; q += 16) st16v(out + q, ring_ld(ring, q));

@@ -41,6 +41,9 @@ int main(int argc, char **argv) {
     alignas(16) static uint8_t ring[1024];
     for (uint64_t s = 0; s < count; s++)
         if (!(hw ? ez::ring_one<true>(a, s, ring + 16) : ez::ring_one<false>(a, s, ring + 16))) size[s] = ~0ull;  // front guard
+#ifndef __HIP_DEVICE_COMPILE__
+    std::fprintf(stderr, "iterations per stream %.1f\n", (double)ez::g_ring_iters / (double)(count ? count : 1));
+#endif
     FILE *fo = std::fopen(argv[4], "wb");
     for (uint64_t s = 0; s < count; s++)
         if (size[s] != ~0ull) std::fwrite(out.data() + out_off[s], 1, size[s], fo);
