@@ -492,9 +492,20 @@ class Reader:
         """True while the Reads are served from the whole-stream decode (ez_reader_whole_decoded)."""
         return bool(_lib().ez_reader_whole_decoded(self._h))
 
+    @property
+    def ahead_count(self) -> int:
+        """Read-aheads this NewReader(io.Reader) handle has made (ez_reader_ahead_count)."""
+        L = _lib()
+        L.ez_reader_ahead_count.restype = C.c_int64
+        L.ez_reader_ahead_count.argtypes = [C.c_void_p]
+        return int(L.ez_reader_ahead_count(self._h))
+
     def Read(self, n: int):  # reader.go:116-141
         L = _lib()
-        L.ez_reader_configure(self._h, self.BlockSizeLimit, int(self.RequireMagic), int(self.SkipUnsupportedMeta))
+        cfg = (self.BlockSizeLimit, int(self.RequireMagic), int(self.SkipUnsupportedMeta))
+        if cfg != getattr(self, "_cfg", None):  # (the handle keeps it: one C call per change, not per Read)
+            L.ez_reader_configure(self._h, *cfg)
+            self._cfg = cfg
         p = C.create_string_buffer(max(n, 1))  # (bytes(p[:got]) of a c_uint8 array builds a list: 10x slower)
         got, err = 0, OK
         while got < n and err == OK:

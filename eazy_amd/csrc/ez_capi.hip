@@ -263,6 +263,8 @@ struct ez_writer {
     DBuf ring, ht, dev;
     DBuf recs;             // K1L's match records (single Writes, ez::long_ring_applies)
     HBuf host;             // the same layout, pinned
+    uint8_t *host_dev = nullptr;  // the device's address of `host` (zero-copy Writes), or nullptr
+    void *host_alias_of = nullptr;  // the host.p host_dev was taken for
     hipStream_t stream = nullptr;
 };
 
@@ -396,8 +398,23 @@ int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t
     const size_t o_meta = (n + 15) & ~(size_t)15;
     const size_t o_o = (o_meta + 6 * 8 * k + 15) & ~(size_t)15;
     const size_t total = o_o + bound + 16;
-    if (w->dev.ensure(total) || w->host.ensure(total) || w->recs.ensure((size_t)recmax)) return EZ_EDEVICE;
-    uint8_t *H = w->host.as<uint8_t>(), *D = w->dev.as<uint8_t>();
+    // Writes K1L stages in LDS (read once): the kernels read them, and write the output, in the pinned
+    // host buffer itself -- no host->device and device->host copies (a 100-byte Write's fixed cost)
+    bool zc = true;
+    for (size_t j = 0; j < k; j++) zc = zc && ends[j] - (j ? ends[j - 1] : 0) <= ez::kHandleLdsWrite;
+    if (w->host.ensure(total) || w->recs.ensure((size_t)recmax)) return EZ_EDEVICE;
+    if (zc && w->host_alias_of != w->host.p) {  // the device's address of the pinned buffer
+        void *dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, w->host.p, 0) != hipSuccess) {
+            (void)hipGetLastError();
+            dp = nullptr;
+        }
+        w->host_dev = (uint8_t *)dp;
+        w->host_alias_of = w->host.p;
+    }
+    zc = zc && w->host_dev != nullptr;
+    if (!zc && w->dev.ensure(total)) return EZ_EDEVICE;
+    uint8_t *H = w->host.as<uint8_t>(), *D = zc ? w->host_dev : w->dev.as<uint8_t>();
     memcpy(H, p, n);
     uint64_t *m = (uint64_t *)(H + o_meta);
     size_t boff = 0;
@@ -413,7 +430,7 @@ int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t
         mj[5] = 0;
         boff += b;
     }
-    EZ_HIP(hipMemcpyAsync(D, H, o_meta + 6 * 8 * k, hipMemcpyHostToDevice, w->stream));
+    if (!zc) EZ_HIP(hipMemcpyAsync(D, H, o_meta + 6 * 8 * k, hipMemcpyHostToDevice, w->stream));
     w->tainted = true;  // (cleared when the call completes, or by the reset of a failed one)
     hipError_t he = hipSuccess;
     for (size_t j = 0; j < k && he == hipSuccess; j++) {
@@ -421,7 +438,7 @@ int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t
         const ez::CompressArgs a = long_args(w, D, (uint64_t *)(D + o_meta) + 6 * j, j, len, w->pos + (int64_t)(j ? ends[j - 1] : 0));
         he = ez::launch_long_ring(a, w->recs.as<uint8_t>(), w->stream);
     }
-    if (he == hipSuccess) he = hipMemcpyAsync(H + o_meta, D + o_meta, o_o - o_meta + bound, hipMemcpyDeviceToHost, w->stream);
+    if (he == hipSuccess && !zc) he = hipMemcpyAsync(H + o_meta, D + o_meta, o_o - o_meta + bound, hipMemcpyDeviceToHost, w->stream);
     if (he == hipSuccess) he = hipStreamSynchronize(w->stream);
     if (he != hipSuccess) {
         (void)writer_zero(w);
@@ -643,8 +660,16 @@ struct ez_reader {
     std::vector<uint64_t> brk;              // the Break metas' output positions, ascending
     size_t brk_next = 0;                    // the next one a Read has not reported
     int64_t end_bs = 0, end_pos = 0;        // the Reader's len(r.block) and r.pos after the stream
-    uint8_t *stage = nullptr;               // pinned: a_out[stage_at .. stage_at + stage_n)
+    uint8_t *stage = nullptr;               // pinned: srv[stage_at .. stage_at + stage_n)
     uint64_t stage_at = 0, stage_n = 0;
+    const uint8_t *srv = nullptr;           // the device bytes the Reads are served from (a_out, or a read-ahead's)
+    // read-ahead of a NewReader(io.Reader) handle (whole == 0, ez_reader_read): all the input buffered
+    // at a Read decoded at once; its Reads are then served from srv[a_at .. a_n) (ahead_on stays 0)
+    int s_on = 0;
+    int64_t s_iend = 0;                     // the absolute input position the read-ahead consumed to
+    int64_t s_skip = -1;                    // a read-ahead handed over at this absolute buffer end: none until more input
+    int64_t s_count = 0;                    // read-aheads made (ez_reader_ahead_count)
+    DBuf s_meta, s_ws;
 };
 
 extern "C" int ez_reader_new(int device, ez_reader **out) {
@@ -678,6 +703,8 @@ extern "C" void ez_reader_free(ez_reader *r) {
     r->a_meta.release();
     r->a_ws.release();
     r->a_brk.release();
+    r->s_meta.release();
+    r->s_ws.release();
     if (r->stage) (void)hipHostFree(r->stage);
     if (r->stream) (void)hipStreamDestroy(r->stream);
     delete r;
@@ -698,6 +725,8 @@ extern "C" int ez_reader_reset(ez_reader *r) {
     r->st.ver = ver;
     r->tried = 0;
     r->ahead_on = 0;
+    r->s_on = 0;
+    r->s_skip = -1;
     r->a_n = r->a_at = 0;
     r->brk.clear();
     r->brk_next = 0;
@@ -711,6 +740,8 @@ extern "C" int ez_reader_set_whole(ez_reader *r, int whole) {
 }
 
 extern "C" int ez_reader_whole_decoded(const ez_reader *r) { return r->ahead_on; }
+
+extern "C" int64_t ez_reader_ahead_count(const ez_reader *r) { return r->s_count; }
 
 extern "C" int ez_reader_pending(const ez_reader *r) { return r->st.state != 0 ? 1 : 0; }
 
@@ -819,6 +850,7 @@ int reader_ahead(ez_reader *r, const uint8_t *b, size_t b_len) {
         r->end_bs = (int64_t)m[6];
         r->end_pos = (int64_t)m[7];
         r->stage_at = r->stage_n = 0;
+        r->srv = r->a_out.as<uint8_t>();
         r->ahead_on = 1;
         return 1;
     }
@@ -830,13 +862,13 @@ int ahead_copy(ez_reader *r, uint8_t *p, size_t n) {
         if (r->a_at < r->stage_at || r->a_at >= r->stage_at + r->stage_n) {
             const uint64_t left = r->a_n - r->a_at;
             if (n >= kStage) {
-                if (hipMemcpy(p, r->a_out.as<uint8_t>() + r->a_at, n, hipMemcpyDeviceToHost) != hipSuccess) return EZ_EDEVICE;
+                if (hipMemcpy(p, r->srv + r->a_at, n, hipMemcpyDeviceToHost) != hipSuccess) return EZ_EDEVICE;
                 r->a_at += n;
                 return EZ_OK;
             }
             r->stage_at = r->a_at;
             r->stage_n = left < kStage ? left : kStage;
-            if (hipMemcpy(r->stage, r->a_out.as<uint8_t>() + r->a_at, r->stage_n, hipMemcpyDeviceToHost) != hipSuccess) {
+            if (hipMemcpy(r->stage, r->srv + r->a_at, r->stage_n, hipMemcpyDeviceToHost) != hipSuccess) {
                 r->stage_n = 0;
                 return EZ_EDEVICE;
             }
@@ -849,6 +881,162 @@ int ahead_copy(ez_reader *r, uint8_t *p, size_t n) {
         r->a_at += k;
     }
     return EZ_OK;
+}
+
+constexpr size_t kStreamMin = (size_t)8 << 10;  // buffered input a read-ahead takes at least
+
+// Read-ahead of a NewReader(io.Reader) handle (the README's usage, reader.go:79-86, 116-141, 516-543):
+// at a Read with nothing decoded ahead, every whole token of the buffered input b[i..b_len) is decoded
+// at once on the device -- K2j continuing the stream from the handle's state: the window's history at
+// the head of the decode buffer, a pending literal's bytes put in front, the chain stopping before a
+// token the buffer ends inside of, whose literal bytes there are are output too (reader.go:166-168) --
+// and the Reads are served from that output until it runs out.  Then Read asks for more input exactly
+// where Read by Read would (the whole tokens are consumed, the state is the same), so the io.Reader
+// sees the same calls and the caller the same bytes, Breaks and errors.  A buffer K2j hands over (an
+// error, a MetaReset after output, a distance past the window, ...) is decoded Read by Read until more
+// input arrives.  Returns 1 when the Reads are now served from the read-ahead.
+int stream_ahead(ez_reader *r, const uint8_t *b, size_t b_len, size_t i, int64_t boff) {
+    ez::DecodeState &st = r->st;
+    const int64_t bend = boff + (int64_t)b_len;
+    if (r->require_magic || r->skip_meta || b_len < i + kStreamMin || b_len > ((size_t)1 << 28) || bend == r->s_skip) return 0;
+    if (st.state == 'c' || st.ver != 0 || st.bs > ((int64_t)1 << 30)) return 0;  // (mid-copy: after a Read that filled p)
+    const size_t H = (size_t)st.hist, nin = b_len - i;
+    // a pending literal (r.state 'l'): its next bytes are the input's first
+    const size_t k = st.state == 'l' ? (st.len < (int64_t)nin ? (size_t)st.len : nin) : 0;
+    const size_t n2 = nin - k;  // the input K2j decodes (none when the literal takes it all)
+    const size_t ws = ez_decompress_workspace(1);
+    if (r->in.ensure(n2 + 64) || r->s_meta.ensure(256) || r->s_ws.ensure(ws) || r->a_brk.ensure(8 * (kAheadBrk + 1))) return 0;
+    if (!r->stage && hipHostMalloc((void **)&r->stage, kStage, hipHostMallocDefault) != hipSuccess) {
+        r->stage = nullptr;
+        return 0;
+    }
+    if (n2 && hipMemcpyAsync(r->in.p, b + i + k, n2, hipMemcpyHostToDevice, r->stream) != hipSuccess) return 0;
+    size_t cap = n2 ? 8 * n2 + 4096 : 0;
+    for (;;) {
+        if (cap > kAheadMax) return 0;
+        DBuf &cur = r->obuf[r->cur];
+        if (cur.cap < H + k + cap + 64) {  // grow, keeping the history at the head
+            DBuf nbuf;
+            if (nbuf.ensure(H + k + cap + 64)) return 0;
+            if (H && hipMemcpyAsync(nbuf.p, cur.p, H, hipMemcpyDeviceToDevice, r->stream) != hipSuccess) return 0;
+            if (hipStreamSynchronize(r->stream) != hipSuccess) return 0;
+            cur.release();
+            cur = nbuf;
+            nbuf.p = nullptr;
+            nbuf.cap = 0;
+        }
+        uint8_t *o = cur.as<uint8_t>();
+        if (k && hipMemcpyAsync(o + H, b + i, k, hipMemcpyHostToDevice, r->stream) != hipSuccess) return 0;
+        // [in_off 2][out_off 2][out_size][status][end_state 5][slow count (u32)]
+        uint64_t m[12] = {0, (uint64_t)n2, (uint64_t)(H + k), (uint64_t)(H + k + cap), 0, 0, 0, 0, 0, 0, 0, 0};
+        uint64_t nbrk = 0;
+        if (n2) {
+            uint64_t *dm = r->s_meta.as<uint64_t>();
+            if (hipMemcpyAsync(dm, m, sizeof m, hipMemcpyHostToDevice, r->stream) != hipSuccess) return 0;
+            if (hipMemsetAsync(r->a_brk.p, 0, 8, r->stream) != hipSuccess) return 0;
+            if (hipMemsetAsync(r->s_ws.p, 0, 4, r->stream) != hipSuccess) return 0;
+            ez::DecompressArgs a{};
+            a.in = r->in.as<uint8_t>();
+            a.in_off = dm;
+            a.out = o;
+            a.out_off = dm + 2;
+            a.out_size = dm + 4;
+            a.status = (int32_t *)(dm + 5);
+            a.end_state = (int64_t *)(dm + 6);
+            a.breaks = r->a_brk.as<uint64_t>();
+            a.breaks_cap = kAheadBrk;
+            a.count = 1;
+            a.block_size_limit = r->limit;
+            a.slow = r->s_ws.as<uint32_t>();
+            a.max_out = cap;
+            a.in_bytes = n2;
+            a.out_bytes = cap;
+            a.c_on = 1;
+            a.c_bsl = st.bs == 0 ? -1 : __builtin_ctzll((uint64_t)st.bs);
+            a.c_hist = H + k;
+            a.c_pos0 = st.pos + (int64_t)k;
+            {
+                ReaderJws &J = reader_jws(r->device);
+                std::lock_guard<std::mutex> lk(J.mu);
+                const uint64_t need = ez::jump_workspace_bytes(1, n2, cap + H + k + 16);
+                if (J.buf.ensure(need)) return 0;
+                a.jws = J.buf.p;
+                a.jws_cap = J.buf.cap;
+                if (ez::launch_decompress_jump(a, r->stream) != hipSuccess) return 0;
+                if (hipMemcpyAsync(m, dm, sizeof m, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
+                if (hipMemcpyAsync(&nbrk, r->a_brk.p, 8, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
+                uint32_t slow = 0;
+                if (hipMemcpyAsync(&slow, r->s_ws.p, 4, hipMemcpyDeviceToHost, r->stream) != hipSuccess) return 0;
+                if (hipStreamSynchronize(r->stream) != hipSuccess) return 0;
+                if (slow) {
+                    if ((int64_t)m[6] == -2 && cap < kAheadMax) {  // the slot was too small
+                        cap = cap < kAheadMax / 4 ? 4 * cap : kAheadMax;
+                        continue;
+                    }
+                    r->s_skip = bend;  // handed over: Read by Read until more input arrives
+                    return 0;
+                }
+            }
+            if (nbrk > kAheadBrk) {
+                r->s_skip = bend;
+                return 0;
+            }
+        }
+        // the chain's stop and a literal the input ends inside of
+        const int64_t total = n2 ? (int64_t)m[4] : 0;
+        const int64_t stop = n2 ? (int64_t)m[8] : 0, tj = n2 ? (int64_t)m[9] : 0, tL = n2 ? (int64_t)m[10] : 0;
+        int64_t tail = 0;
+        if (tj > 0) {
+            tail = (int64_t)n2 - stop - tj < tL ? (int64_t)n2 - stop - tj : tL;
+            if (tail > 0 &&
+                hipMemcpyAsync(o + H + k + total, r->in.as<uint8_t>() + stop + tj, (size_t)tail, hipMemcpyDeviceToDevice, r->stream) != hipSuccess)
+                return 0;
+        }
+        try {
+            r->brk.resize((size_t)nbrk);
+        } catch (...) {
+            return 0;
+        }
+        if (nbrk && hipMemcpy(r->brk.data(), r->a_brk.as<uint64_t>() + 1, 8 * nbrk, hipMemcpyDeviceToHost) != hipSuccess) return 0;
+        for (auto &x : r->brk) x += k;  // (positions in the served bytes: the pending literal's come first)
+        std::sort(r->brk.begin(), r->brk.end());
+        // the Reader's state after the last whole token (or inside the literal the input ends in)
+        const int64_t out_n = (int64_t)k + total + tail;
+        ez::DecodeState ns = st;
+        if (n2) ns.bs = (int64_t)m[6];
+        ns.pos = st.pos + out_n;
+        if (n2 == 0) {  // the pending literal took the whole input
+            ns.len = st.len - (int64_t)k;
+            ns.state = ns.len == 0 ? 0 : 'l';
+        } else if (tj > 0) {
+            ns.state = 'l';
+            ns.len = tL - tail;
+        } else {
+            ns.state = 0;
+            ns.len = 0;
+        }
+        ns.hist = ns.bs == 0 ? 0 : (ns.pos < ns.bs ? ns.pos : ns.bs);
+        // the next decode's history: the window's last hist bytes, at the head of the other buffer
+        const size_t H2 = (size_t)ns.hist;
+        if (H2 > H + (size_t)out_n) return 0;  // (cannot happen: the history is decoded output)
+        DBuf &nxt = r->obuf[r->cur ^ 1];
+        if (nxt.cap < H2 + 16) {
+            if (hipStreamSynchronize(r->stream) != hipSuccess || nxt.ensure(H2 + 16)) return 0;
+        }
+        if (H2 && hipMemcpyAsync(nxt.p, o + H + out_n - H2, H2, hipMemcpyDeviceToDevice, r->stream) != hipSuccess) return 0;
+        if (hipStreamSynchronize(r->stream) != hipSuccess) return 0;
+        r->cur ^= 1;  // (the served bytes stay in this buffer; the next decode writes the other)
+        st = ns;
+        r->srv = o + H;
+        r->a_n = (uint64_t)out_n;
+        r->a_at = 0;
+        r->brk_next = 0;
+        r->stage_at = r->stage_n = 0;
+        r->s_iend = boff + (int64_t)(n2 == 0 || tj > 0 ? b_len : i + k + (size_t)stop);
+        r->s_on = 1;
+        r->s_count++;
+        return 1;
+    }
 }
 
 // Input after the decoded stream (a Reader set after NewReaderBytes, so more() supplied more): the
@@ -894,6 +1082,24 @@ extern "C" int ez_reader_read(ez_reader *r, const uint8_t *b, size_t b_len, size
     if (r->ahead_on && r->a_at == r->a_n && r->brk_next == r->brk.size() && (uint64_t)boff + b_len > r->a_blen) {
         // the stream is served and input follows it: Read by Read from the Reader's state at its end
         if (ahead_leave(r) != EZ_OK) return EZ_EDEVICE;
+    }
+    // NewReader(io.Reader): the buffered input decoded ahead, the Reads served from it
+    if (!r->whole && !r->s_on) (void)stream_ahead(r, b, b_len, i, boff);
+    if (r->s_on) {
+        const bool at_brk = r->brk_next < r->brk.size();
+        const uint64_t lim = at_brk ? r->brk[r->brk_next] : r->a_n;
+        const uint64_t left = lim - r->a_at;
+        const size_t m = p_len < left ? p_len : (size_t)left;
+        if (m && ahead_copy(r, p, m) != EZ_OK) return EZ_EDEVICE;
+        *n = m;
+        *i_out = (size_t)(r->s_iend - boff);  // (only read back when this returns ErrShortBuffer)
+        if (m == p_len) return EZ_OK;
+        if (at_brk) {
+            r->brk_next++;
+            return EZ_EBREAK;
+        }
+        r->s_on = 0;  // served: Read asks for more input where Read by Read would
+        return EZ_ESHORTBUF;
     }
     if (r->ahead_on) {
         // up to the next Break (reader.go:312-313: Read returns the bytes before it with ErrBreak, and a

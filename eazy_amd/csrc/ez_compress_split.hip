@@ -1384,6 +1384,7 @@ struct RingSrc {
 // at most kLdsWrite bytes): lds + kLdsRing + y holds position y for -rl <= y < n + 64 (zeros past
 // the Write); the window's bytes and the candidates' come from there, anything else from RingSrc.
 constexpr int32_t kLdsRing = 32768, kLdsWrite = 49152;
+static_assert(kLdsWrite == (int32_t)kHandleLdsWrite, "the handle path's zero-copy bound is K1L's LDS-staged Write");
 typedef uint64_t __attribute__((aligned(1))) u64_ua;
 typedef uint32_t __attribute__((aligned(1))) u32_ua;
 struct LdsSrc {

@@ -45,12 +45,13 @@
 namespace ez {
 namespace {
 
-constexpr int32_t kJC = 2048;                        // compressed bytes per chunk
+constexpr int32_t kJC = 1024;                        // compressed bytes per chunk
 constexpr int32_t kJW = kJC / 32;                    // bitmap words per chunk
 constexpr uint32_t kJGap = 0xffffffffu;              // ptr: not a byte of any stream's output
 constexpr uint32_t kJZero = 0xfffffffeu;             // ptr: a zero byte of the history before the stream
 constexpr uint32_t kJCopy = 0x80000000u;             // JTok.kd: a copy (distance in the low bits; 0: zero region)
-constexpr int kJPasses = 34;                         // pointer-jumping passes queued (chains up to 2^34)
+constexpr int kJPasses = 34;                         // pointer-jumping passes at most (chains up to 2^34)
+constexpr uint32_t kJRec = kJC / 2 + 2;              // token records of a chunk at most (a token takes >= 2 bytes)
 
 struct JHead {
     uint32_t chunk0, nchunk;  // the stream's chunks
@@ -59,7 +60,16 @@ struct JHead {
     uint64_t total;           // output bytes
     uint64_t ntok;            // token records
     uint64_t tok0;            // its first record
+    // (c_on) where the chain stops: the input consumed by whole tokens, and a literal starting there
+    // whose body runs past the input (its header length, its length; 0: none)
+    int32_t tstop, tj;
+    int64_t tL;
 };
+
+// the ptr array's first byte: out_off[0] less the continuation's history, rounded down to 16 bytes
+__device__ __forceinline__ uint64_t jg0(const DecompressArgs &A) {
+    return (A.out_off[0] - (A.c_on ? A.c_hist : 0)) & ~15ull;
+}
 
 struct JTok {
     uint32_t dst, L, kd, src;  // output position, length, kJCopy | distance (or 0: literal), literal's input position
@@ -75,6 +85,8 @@ struct JWork {
     uint64_t *ctbase, *cobase;
     JTok *tok;
     uint64_t tok_cap;
+    JTok *ltok;         // kj_tok's records, chunk-local (kJRec per chunk, dst from the chunk's output start)
+    uint32_t *cmaxd;    // the longest copy distance of a chunk
     uint32_t *ptr;
     uint32_t *pass;     // [kJPasses]: the pass changed something; [kJPasses]: token records allocated
 };
@@ -106,6 +118,88 @@ __device__ __forceinline__ int32_t jadv(const uint8_t *b, int32_t p, int32_t nb,
     return r == kParseHandOver ? -1 : t.adv;
 }
 
+// The walks of kj_spec / kj_count / kj_emit read their chunk's tokens from LDS: a block's 64 chunks are
+// consecutive in the batch's input (a stream's chunks follow each other, and so do the streams), so
+// the block stages the bytes from its first chunk's start to 16 past its last chunk's end with
+// coalesced 16-byte loads, and every token step is then an LDS read instead of a dependent global
+// load (a 61 KiB stream: the three walks 840 -> see DESIGN §4 K2j).
+// kj_spec starts each chunk's speculative parse kJWarm bytes before it (positions before the chunk are
+// not recorded), so that its chain has usually met the true one by the chunk's start: kj_verify's
+// walks then end at their first step and kj_fix has (almost) nothing to redo
+constexpr int32_t kJWarm = 256;
+constexpr int32_t kJStage = 64 * kJC + kJWarm + 32;  // LDS bytes of a block's staged input
+struct JStage {
+    uint8_t *lds;
+    uint64_t base;  // batch offset of lds[0]
+    __device__ __forceinline__ V16 at(uint64_t y) const {  // 16 bytes at batch offset y (staged)
+        const uint8_t *q = lds + (y - base);
+        typedef uint64_t __attribute__((aligned(1))) u64u;
+        return V16{*(const u64u *)q, *(const u64u *)(q + 8)};
+    }
+};
+// stage [first chunk's start, last chunk's end + 16) of the batch (zeros past its end); every lane of
+// the block calls it (a lane without a chunk passes live = false); returns the block's staging
+__device__ __forceinline__ JStage kj_stage(const DecompressArgs &A, bool live, uint64_t start, uint64_t end, uint8_t *lds) {
+    __shared__ uint64_t ext[2];
+    if (threadIdx.x == 0) {
+        ext[0] = ~0ull;
+        ext[1] = 0;
+    }
+    __syncthreads();
+    if (live) {
+        atomicMin((unsigned long long *)&ext[0], (unsigned long long)start);
+        atomicMax((unsigned long long *)&ext[1], (unsigned long long)end);
+    }
+    __syncthreads();
+    const uint64_t base = ext[0], stop = ext[1] + 16, total = A.in_off[A.count];
+    if (base < stop) {
+        for (uint64_t o = (uint64_t)threadIdx.x * 16; base + o < stop; o += (uint64_t)blockDim.x * 16) {
+            const uint64_t y = base + o;
+            const V16 v = y + 16 <= total ? ld16v(A.in + y) : ld_clamped(A.in + y, A.in, A.in + total);
+            typedef uint64_t __attribute__((aligned(8))) u64a;
+            *(u64a *)(lds + o) = v.lo;
+            *(u64a *)(lds + o + 8) = v.hi;
+        }
+    }
+    __syncthreads();
+    return JStage{lds, base};
+}
+// jadv on staged bytes (the token at stream position p; b0 = the stream's batch offset)
+__device__ __forceinline__ int32_t jadv_s(const JStage &S, uint64_t b0, int32_t p, int32_t nb, int32_t lim32, int64_t limit, K2Tok &t,
+                                          int &r, bool partial = false) {
+    r = k2_scan(S.at(b0 + (uint64_t)p), p, nb, lim32, limit, t, partial);
+    return r == kParseHandOver ? -1 : t.adv;
+}
+
+// The input bytes the token (or padding run, or meta) at the 16 bytes h takes, for the speculative
+// walks (kj_spec, kj_prop): the same advance as k2_scan for every form it accepts, from 32-bit
+// arithmetic on the header's first 8 bytes and no checks (a form k2_scan hands over advances by some
+// amount >= 1 here; kj_count's full parse of the true chain then hands the stream over)
+__device__ __forceinline__ int32_t jadv_fast(V16 h) {
+    const uint32_t w0 = (uint32_t)h.lo, w1 = (uint32_t)(h.lo >> 32);
+    const uint32_t t0 = w0 & 0xff, l7 = t0 & 0x7f;
+    if (t0 == 0) return h.lo ? (int32_t)(__builtin_ctzll(h.lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
+    if (t0 == 0x80) {
+        const uint32_t ml = (w0 >> 8) & 7;
+        return 2 + (ml == 7 ? 0 : (1 << ml));
+    }
+    const uint32_t ln = l7 >= 124 ? 1u << (l7 - 124 < 2 ? l7 - 124 : 2) : 0u;  // extra length bytes
+    const uint32_t j = 1 + ln;
+    if (!(t0 & 0x80)) {  // literal: the tag, then L bytes
+        const uint32_t lx = __builtin_amdgcn_alignbyte(w1, w0, 1);  // bytes 1..4
+        const uint32_t lmask = ln == 4 ? 0x3fffffffu : (1u << (8 * ln)) - 1;
+        const uint32_t L = l7 >= 124 ? 124u + (l7 >= 125 ? 256u : 0u) + (l7 >= 126 ? 65536u : 0u) + (lx & lmask) : l7;
+        const uint32_t adv = j + L;
+        return adv > 0x7fffffffu ? 0x7fffffff : (int32_t)adv;
+    }
+    // copy: the tag, the long prefix (0xff) if any, the offset byte and its 1, 2 or 4 extra bytes
+    const uint32_t bj = (uint32_t)(h.lo >> (8 * j)) & 0xff;  // (j <= 5)
+    const uint32_t jo = j + (bj == 0xff ? 1u : 0u);
+    const uint32_t o = (uint32_t)(h.lo >> (8 * jo)) & 0xff;  // (jo <= 6)
+    const uint32_t on = o >= 252 ? 1u << (o - 252 < 2 ? o - 252 : 2) : 0u;
+    return (int32_t)(jo + 1 + on);
+}
+
 // ---- 0: chunks per stream
 __global__ __launch_bounds__(1024) void kj_init(DecompressArgs A, JWork W) {
     __shared__ uint32_t part[1024];
@@ -120,8 +214,11 @@ __global__ __launch_bounds__(1024) void kj_init(DecompressArgs A, JWork W) {
             nch = nb == 0 ? 1u : (uint32_t)((nb + kJC - 1) / kJC);
             JHead h{};
             // (pointers are 32-bit offsets from the batch's first output slot, rounded down to 16 bytes)
-            h.state = (nb >= (1ull << 31) || cap >= (1ull << 32) - 2 || A.out_off[s + 1] - (A.out_off[0] & ~15ull) >= (1ull << 32) - 2) ? 1u : 0u;
+            h.state = (nb >= (1ull << 31) || cap >= (1ull << 32) - 2 || A.out_off[s + 1] - jg0(A) >= (1ull << 32) - 2) ? 1u : 0u;
             h.bsl = -1;
+            h.tstop = (int32_t)(nb < (1ull << 31) ? nb : 0);
+            h.tj = 0;
+            h.tL = 0;
             h.nchunk = nch;
             W.head[s] = h;
         }
@@ -144,129 +241,205 @@ __global__ __launch_bounds__(1024) void kj_init(DecompressArgs A, JWork W) {
     if (t == 0) W.cbase[A.count] = carry;
 }
 
-// ---- 1a: speculative parse of each chunk from its first byte: the positions visited, the exit
+// ---- 1a: speculative parse of each chunk (from kJWarm bytes before it): the positions it visits in the
+// chunk, and its exit
 __global__ __launch_bounds__(64) void kj_spec(DecompressArgs A, JWork W) {
     __shared__ uint32_t bm[64][kJW + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kJStage];
     const uint32_t lane = threadIdx.x;
     const uint32_t total = W.cbase[A.count];
     const uint32_t c = blockIdx.x * 64 + lane;
-    if (c >= total) return;
-    const uint32_t s = chunk_stream(W.cbase, (uint32_t)A.count, c);
-    if (W.head[s].state) return;
-    const uint8_t *b = A.in + A.in_off[s], *lo = A.in, *hi = A.in + A.in_off[A.count];
+    bool live = c < total;
+    const uint32_t s = live ? chunk_stream(W.cbase, (uint32_t)A.count, c) : 0;
+    live = live && !W.head[s].state;
+    const uint64_t b0 = A.in_off[s];
     const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
-    const int64_t limit = A.block_size_limit;
-    const int32_t lim32 = limit == 0 || limit > 0x7fffffff ? 0x7fffffff : (int32_t)limit;
     const int32_t c0 = (int32_t)(c - W.cbase[s]) * kJC, ce = c0 + kJC < nb ? c0 + kJC : nb;
+    const int32_t w0 = c0 > kJWarm ? c0 - kJWarm : 0;
+    const JStage S = kj_stage(A, live, b0 + (uint64_t)w0, b0 + (uint64_t)ce, stage);
+    if (!live) return;
     for (int k = 0; k < kJW; k++) bm[lane][k] = 0;
-    int32_t p = c0;
+    int32_t p = w0;
+    while (p < c0) p += jadv_fast(S.at(b0 + (uint64_t)p));  // (the warm-up: nothing recorded)
     while (p < ce) {
         bm[lane][(p - c0) >> 5] |= 1u << ((p - c0) & 31);
-        K2Tok t;
-        int r;
-        const int32_t a = jadv(b, p, nb, lim32, limit, lo, hi, t, r);
-        p += a > 0 ? a : 1;
+        p += jadv_fast(S.at(b0 + (uint64_t)p));
     }
     uint32_t *g = W.bits + (uint64_t)c * kJW;
     for (int k = 0; k < kJW; k++) g[k] = bm[lane][k];
     W.sexit[c] = (uint32_t)p;
 }
 
-// ---- 1b: the true entry of every chunk, 64 chunks per step (wave per stream)
-__global__ __launch_bounds__(64) void kj_prop(DecompressArgs A, JWork W) {
+// ---- 1b: the true entry of every chunk.  Chunk c's entry is its predecessor's speculative exit when
+// the predecessor's speculative chain merged with the true chain inside it (a wrong start meets the
+// true chain within ~110 bytes on the logs, 99 % within 1 KiB); every chunk checks that at once
+// (kj_verify: thread per chunk, walking the true chain from that entry until a position its own
+// speculative parse visited -- its speculative exit is then its true exit -- or its end), and a wave
+// per stream then redoes, in order, only the chunks whose predecessor did not merge (kj_fix).
+// texit[c]: chunk c's true exit given that entry; entry[c]: the entry the check assumed
+__device__ __forceinline__ int32_t kj_walk_true(const JWork &W, uint32_t cg, const uint8_t *b, int32_t a, int32_t cs, int32_t ce,
+                                                const uint8_t *lo, const uint8_t *hi) {
+    const uint32_t *g = W.bits + (uint64_t)cg * kJW;
+    int32_t q = a;
+    while (q < ce) {
+        if ((g[(q - cs) >> 5] >> ((q - cs) & 31)) & 1u) return (int32_t)W.sexit[cg];  // merged: its exit is the chain's
+        q += jadv_fast(jbytes(b, q, lo, hi));
+    }
+    return q;
+}
+
+__global__ __launch_bounds__(64) void kj_verify(DecompressArgs A, JWork W) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kJStage];
+    const uint32_t total = W.cbase[A.count];
+    const uint32_t c = blockIdx.x * 64 + threadIdx.x;
+    bool live = c < total;
+    const uint32_t s = live ? chunk_stream(W.cbase, (uint32_t)A.count, c) : 0;
+    live = live && !W.head[s].state;
+    const uint64_t b0 = A.in_off[s];
+    const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+    const uint32_t k = c - W.cbase[s];
+    const int32_t c0 = (int32_t)k * kJC, ce = c0 + kJC < nb ? c0 + kJC : nb;
+    const JStage S = kj_stage(A, live, b0 + (uint64_t)c0, b0 + (uint64_t)ce, stage);
+    if (!live) return;
+    const int32_t a = k == 0 ? 0 : (int32_t)W.sexit[c - 1];
+    int32_t x;
+    if (k == 0) {
+        x = (int32_t)W.sexit[c];  // (chunk 0's speculation starts at the stream's start: it is the true chain)
+    } else if (a >= ce) {
+        x = a;  // an entry past the chunk (inside a long token) passes through
+    } else {
+        const uint32_t *g = W.bits + (uint64_t)c * kJW;
+        int32_t q = a < c0 ? c0 : a;  // (a < c0 cannot happen: a speculative exit is >= its chunk's end)
+        x = -1;
+        while (q < ce) {
+            if ((g[(q - c0) >> 5] >> ((q - c0) & 31)) & 1u) {
+                x = (int32_t)W.sexit[c];
+                break;
+            }
+            q += jadv_fast(S.at(b0 + (uint64_t)q));
+        }
+        if (x < 0) x = q;
+    }
+    W.entry[c] = (uint32_t)a;
+    W.cnt[c] = (uint32_t)x;  // (the true exit; kj_count overwrites cnt with the token count)
+}
+
+__global__ __launch_bounds__(64) void kj_fix(DecompressArgs A, JWork W) {
     const uint32_t s = blockIdx.x, lane = threadIdx.x;
     JHead &H = W.head[s];
     if (H.state) return;
     const uint8_t *b = A.in + A.in_off[s], *lo = A.in, *hi = A.in + A.in_off[A.count];
     const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
-    const int64_t limit = A.block_size_limit;
-    const int32_t lim32 = limit == 0 || limit > 0x7fffffff ? 0x7fffffff : (int32_t)limit;
     const uint32_t c00 = H.chunk0, nch = H.nchunk;
-    uint32_t k = 0;     // the first chunk whose entry is not known yet
-    int32_t e = 0;      // its entry (the true chain's first position at or after its first byte)
-    bool bad = false;
+    uint32_t *texit = W.cnt;
+    // chunks [0, k) are right; chunk j's entry is right iff its predecessor's true exit is the
+    // speculative exit it assumed.  The true exit of the chunk fixed last is kept in a register
+    // (fx_at, fx_val): this kernel's own stores are not read back.
+    uint32_t k = 1, fx_at = ~0u;
+    int32_t fx_val = 0;
     while (k < nch) {
         const uint32_t j = k + lane;
-        const bool mine = j < nch;
-        const int32_t cs = (int32_t)j * kJC, ce = cs + kJC < nb ? cs + kJC : nb;
-        int32_t a = lane == 0 ? e : (mine ? (int32_t)W.sexit[c00 + j - 1] : 0);
-        // walk the true chain from a until a position the speculative parse visited, or the chunk's end
-        int32_t q = a;
-        bool lbad = false, synced = false;
-        if (mine && a < ce && a >= cs) {
-            const uint32_t *g = W.bits + (uint64_t)(c00 + j) * kJW;
-            while (q < ce) {
-                if ((g[(q - cs) >> 5] >> ((q - cs) & 31)) & 1u) {
-                    synced = true;
-                    break;
-                }
-                K2Tok t;
-                int r;
-                const int32_t ad = jadv(b, q, nb, lim32, limit, lo, hi, t, r);
-                lbad |= ad < 0;
-                q += ad > 0 ? ad : 1;
+        bool bad = false;
+        if (j < nch) {
+            const uint32_t tx = j - 1 == fx_at ? (uint32_t)fx_val : texit[c00 + j - 1];
+            bad = tx != W.sexit[c00 + j - 1];
+        }
+        const uint64_t m = __ballot(bad);
+        if (m == 0) {
+            k += 64;
+            continue;
+        }
+        const uint32_t jf = k + (uint32_t)__builtin_ctzll(m);  // the first chunk entered wrongly
+        const int32_t e = jf - 1 == fx_at ? fx_val : (int32_t)texit[c00 + jf - 1];  // its true entry
+        // an entry past chunk jf (inside a long token): no token starts in the chunks it covers
+        uint32_t kw = jf;
+        if (e >= nb || e >= (int32_t)(jf + 1) * kJC) {
+            kw = e >= nb ? nch : (uint32_t)(e / kJC);
+            for (uint32_t x = jf + lane; x < kw; x += 64) {
+                W.entry[c00 + x] = (uint32_t)e;
+                texit[c00 + x] = (uint32_t)e;
+            }
+            if (kw >= nch) {
+                fx_at = nch - 1;
+                fx_val = e;
+                break;
             }
         }
-        // a chunk whose entry lies past it (inside a long token), or one the chains do not meet in,
-        // ends the step: its exit is the position the walk reached
-        const uint64_t stop = __ballot(mine && !synced);
-        const uint32_t js = stop ? (uint32_t)__builtin_ctzll(stop) : 64u;
-        const uint32_t nw = js < 64 ? js + 1 : (nch - k < 64 ? nch - k : 64);
-        if (lane < nw && mine) W.entry[c00 + j] = (uint32_t)a;
-        if (__ballot(lane < nw && mine && lbad)) bad = true;
-        if (js < 64) {
-            e = __shfl(q > a ? q : a, (int)js);  // (an entry past the chunk passes through)
-        } else {
-            e = (int32_t)W.sexit[c00 + k + nw - 1];
+        // chunk kw holds e: the true chain from there (one lane; rare)
+        int32_t x = 0;
+        if (lane == 0) {
+            const int32_t cs = (int32_t)kw * kJC, ce = cs + kJC < nb ? cs + kJC : nb;
+            x = kj_walk_true(W, c00 + kw, b, e, cs, ce, lo, hi);
+            W.entry[c00 + kw] = (uint32_t)e;
+            texit[c00 + kw] = (uint32_t)x;
         }
-        k += nw;
-        // chunks inside a long token: no token starts there
-        if (k < nch && e >= (int32_t)(k + 1) * kJC) {
-            const uint32_t k2 = e >= nb ? nch : (uint32_t)(e / kJC);
-            for (uint32_t x = k + lane; x < k2; x += 64) W.entry[c00 + x] = (uint32_t)e;
-            k = k2;
-        }
-        if (bad) break;
+        fx_at = kw;
+        fx_val = __shfl(x, 0);
+        k = kw + 1;
     }
-    // the chain must end exactly at the stream's end (else the last token runs past the input)
-    if (lane == 0 && (bad || e != nb)) H.state = 1;
+    // the chain must end exactly at the stream's end (else the last token runs past the input; a
+    // Reader's read-ahead, c_on, stops before that token: kj_count finds it)
+    const int32_t last = nch - 1 == fx_at ? fx_val : (int32_t)texit[c00 + nch - 1];
+    if (lane == 0 && (A.c_on ? last < nb : last != nb)) H.state = 1;
 }
 
-// ---- 2a: the true chain of each chunk: tokens, output bytes, forms and metas
-__global__ __launch_bounds__(64) void kj_count(DecompressArgs A, JWork W) {
+// ---- 2a: the true chain of each chunk, parsed once: tokens, output bytes, forms and metas, a record
+// per token (chunk-local: output positions from the chunk's start; kj_place moves them into the
+// stream's array once the chunks' positions are known), the longest distance, Break positions
+__global__ __launch_bounds__(64) void kj_tok(DecompressArgs A, JWork W) {
+    __shared__ __attribute__((aligned(16))) uint8_t stage[kJStage];
     const uint32_t total = W.cbase[A.count];
     const uint32_t c = blockIdx.x * 64 + threadIdx.x;
-    if (c >= total) return;
-    const uint32_t s = chunk_stream(W.cbase, (uint32_t)A.count, c);
-    if (W.head[s].state) return;
-    const uint8_t *b = A.in + A.in_off[s], *lo = A.in, *hi = A.in + A.in_off[A.count];
+    bool live = c < total;
+    const uint32_t s = live ? chunk_stream(W.cbase, (uint32_t)A.count, c) : 0;
+    live = live && !W.head[s].state;
+    const uint64_t b0 = A.in_off[s];
     const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+    const int32_t c0 = (int32_t)(c - W.cbase[s]) * kJC, ce = c0 + kJC < nb ? c0 + kJC : nb;
+    const JStage S = kj_stage(A, live, b0 + (uint64_t)c0, b0 + (uint64_t)ce, stage);
+    if (!live) return;
     const int64_t limit = A.block_size_limit;
     const int32_t lim32 = limit == 0 || limit > 0x7fffffff ? 0x7fffffff : (int32_t)limit;
-    const int32_t c0 = (int32_t)(c - W.cbase[s]) * kJC, ce = c0 + kJC < nb ? c0 + kJC : nb;
     int32_t p = (int32_t)W.entry[c];
-    uint32_t n = 0, fl = 0;
+    uint32_t n = 0, fl = 0, maxd = 0;
     uint64_t out = 0;
+    const bool partial = A.c_on != 0;
+    JTok *rec = W.ltok + (uint64_t)c * kJRec;
     while (p < ce) {
         K2Tok t;
         int r;
-        const int32_t ad = jadv(b, p, nb, lim32, limit, lo, hi, t, r);
-        if (ad < 0) {
+        const int32_t ad = jadv_s(S, b0, p, nb, lim32, limit, t, r, partial);
+        if (ad < 0 || (r == kParseToken && n >= kJRec)) {
             fl |= kJFBad;
+            break;
+        }
+        if (r == kScanTail) {  // the chain stops here (one chunk of the stream meets it)
+            JHead &H = W.head[s];
+            H.tstop = p;
+            H.tj = t.adv ? t.j : 0;
+            H.tL = t.adv ? t.L : 0;
             break;
         }
         if (r == kScanReset) {
             fl |= (out ? kJFResetLate : 0) | kJFReset | (n == 0 ? 0 : kJFOutFirst);
             fl = (fl & 0xffu) | (t.marg << 8);
         } else if (r == kParseToken) {
-            n++;
+            rec[n++] = JTok{(uint32_t)out, (uint32_t)t.L, t.cp ? (kJCopy | t.D) : 0u, (uint32_t)(p + t.j)};
+            maxd = t.cp && t.D > maxd ? t.D : maxd;
             out += (uint64_t)t.L;
+        } else if (r == kParseSkip && A.breaks) {  // (one-stream batches) a Break: (chunk, local position)
+            const V16 h = S.at(b0 + (uint64_t)p);
+            if (((uint32_t)h.lo & 0xffffu) == (0x80u | ((kMetaBreak | kMetaLen0) << 8))) {
+                const uint64_t at = atomicAdd((unsigned long long *)A.breaks, 1ull);
+                if (at < A.breaks_cap) A.breaks[1 + at] = ((uint64_t)c << 32) | (out & 0xffffffffull);
+            }
         }
         p += ad;
     }
     W.cnt[c] = n;
     W.cout[c] = out;
     W.cflag[c] = fl;
+    W.cmaxd[c] = maxd;
 }
 
 // ---- 2b: token and output positions of the chunks; the stream's checks (wave per stream)
@@ -276,13 +449,18 @@ __global__ __launch_bounds__(64) void kj_scan(DecompressArgs A, JWork W, uint64_
     if (H.state) return;
     const uint32_t c00 = H.chunk0, nch = H.nchunk;
     uint64_t tcarry = 0, ocarry = 0;
-    int32_t bsl = -1;
+    int32_t bsl = A.c_on ? A.c_bsl : -1;  // (a Reader's read-ahead: the window its stream has set)
     bool bad = false;
+    uint32_t maxd = 0;
     for (uint32_t k = 0; k < nch; k += 64) {
         const uint32_t j = k + lane;
         const bool mine = j < nch;
         const uint64_t n = mine ? W.cnt[c00 + j] : 0, o = mine ? W.cout[c00 + j] : 0;
         const uint32_t fl = mine ? W.cflag[c00 + j] : 0;
+        uint32_t md = mine ? W.cmaxd[c00 + j] : 0;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1) md = max(md, (uint32_t)__shfl_xor((int)md, d, 64));
+        maxd = max(maxd, md);
         uint64_t in = n, io = o;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -298,7 +476,7 @@ __global__ __launch_bounds__(64) void kj_scan(DecompressArgs A, JWork W, uint64_
             W.cobase[c00 + j] = obefore;
         }
         // a MetaReset only before any output (and the window it sets is the last such one)
-        const bool rbad = mine && (fl & kJFReset) && (obefore != 0 || (fl & (kJFOutFirst | kJFResetLate)));
+        const bool rbad = mine && (fl & kJFReset) && (obefore != 0 || (fl & (kJFOutFirst | kJFResetLate)) || (A.c_on && A.c_pos0 != 0));
         if (__ballot(rbad || (mine && (fl & kJFBad)))) bad = true;
         const uint64_t rm = __ballot(mine && (fl & kJFReset));
         if (rm) bsl = (int32_t)((__shfl(fl, 63 - __builtin_clzll(rm)) >> 8) & 0xff);
@@ -307,8 +485,14 @@ __global__ __launch_bounds__(64) void kj_scan(DecompressArgs A, JWork W, uint64_
     }
     if (lane != 0) return;
     const uint64_t cap = A.out_off[s + 1] - A.out_off[s];
-    if (!bad && ocarry > 0 && bsl < 0) bad = true;  // "missed meta": a token before the window is set
-    if (!bad && ocarry > cap) {
+    // a literal at the input's end (c_on) whose body runs past it: the bytes there are are output too
+    const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
+    const uint64_t tail = A.c_on && H.tj > 0 ? (uint64_t)min((int64_t)H.tL, (int64_t)(nb - H.tstop - H.tj)) : 0;
+    // "missed meta": a token (or a literal's header) before the window is set
+    if (!bad && (ocarry > 0 || (A.c_on && H.tj > 0)) && bsl < 0) bad = true;
+    // ErrOverflow (reader.go:256-258): a distance past the window -- the exact decoder reports it
+    if (!bad && bsl >= 0 && bsl < 30 && maxd > (1u << bsl)) bad = true;
+    if (!bad && ocarry + tail > cap) {
         bad = true;
         if (A.end_state) A.end_state[0] = -2;  // (a caller that sizes its slot grows it and retries)
     }
@@ -323,42 +507,21 @@ __global__ __launch_bounds__(64) void kj_scan(DecompressArgs A, JWork W, uint64_
     if (bad) H.state = 1;
 }
 
-// ---- 2c: one record per token (lane per chunk); distances against the window; Break positions
-__global__ __launch_bounds__(64) void kj_emit(DecompressArgs A, JWork W) {
-    const uint32_t total = W.cbase[A.count];
-    const uint32_t c = blockIdx.x * 64 + threadIdx.x;
-    if (c >= total) return;
+// ---- 2c: the chunks' records into the stream's array, positions from the stream's start (block per chunk)
+__global__ __launch_bounds__(64) void kj_place(DecompressArgs A, JWork W) {
+    const uint32_t c = blockIdx.x;
+    if (c >= W.cbase[A.count]) return;
     const uint32_t s = chunk_stream(W.cbase, (uint32_t)A.count, c);
-    JHead &H = W.head[s];
+    const JHead &H = W.head[s];
     if (H.state) return;
-    const uint8_t *b = A.in + A.in_off[s], *lo = A.in, *hi = A.in + A.in_off[A.count];
-    const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
-    const int64_t limit = A.block_size_limit;
-    const int32_t lim32 = limit == 0 || limit > 0x7fffffff ? 0x7fffffff : (int32_t)limit;
-    const int32_t c0 = (int32_t)(c - W.cbase[s]) * kJC, ce = c0 + kJC < nb ? c0 + kJC : nb;
-    const int32_t bsl = H.bsl;
-    JTok *rec = W.tok + H.tok0 + W.ctbase[c];
-    uint64_t dst = W.cobase[c];
-    int32_t p = (int32_t)W.entry[c];
-    bool far = false;
-    while (p < ce) {
-        K2Tok t;
-        int r;
-        const int32_t ad = jadv(b, p, nb, lim32, limit, lo, hi, t, r);
-        if (r == kParseToken) {
-            far |= t.cp && bsl < 30 && t.D > (1u << bsl);  // ErrOverflow (reader.go:256-258): the exact decoder
-            *rec++ = JTok{(uint32_t)dst, (uint32_t)t.L, t.cp ? (kJCopy | t.D) : 0u, (uint32_t)(p + t.j)};
-            dst += (uint64_t)t.L;
-        } else if (r == kParseSkip && A.breaks) {
-            const V16 h = jbytes(b, p, lo, hi);
-            if (((uint32_t)h.lo & 0xffffu) == (0x80u | ((kMetaBreak | kMetaLen0) << 8))) {
-                const uint64_t at = atomicAdd((unsigned long long *)A.breaks, 1ull);
-                if (at < A.breaks_cap) A.breaks[1 + at] = dst;
-            }
-        }
-        p += ad > 0 ? ad : 1;
+    const JTok *src = W.ltok + (uint64_t)c * kJRec;
+    JTok *dst = W.tok + H.tok0 + W.ctbase[c];
+    const uint32_t n = W.cnt[c], ob = (uint32_t)W.cobase[c];
+    for (uint32_t k = threadIdx.x; k < n; k += 64) {
+        JTok t = src[k];
+        t.dst += ob;
+        dst[k] = t;
     }
-    if (far) H.state = 1;
 }
 
 // ---- 3: literal and zero bytes, and a pointer for every copied byte (thread per 16 output bytes)
@@ -368,6 +531,7 @@ __global__ __launch_bounds__(64) void kj_emit(DecompressArgs A, JWork W) {
 __device__ __forceinline__ void kj_piece(const DecompressArgs &A, const JWork &W, const JHead &H, uint32_t s, uint64_t q, uint32_t n,
                                          uint64_t g0, uint32_t *by, uint32_t *pt) {
     const uint64_t base = A.out_off[s];
+    const uint32_t hb = A.c_on ? (uint32_t)A.c_hist : 0u;  // history bytes before the output (a copy may read them)
     const uint32_t p0 = (uint32_t)(q - base);
     // the token holding p0: the last record with dst <= p0; the next ones by walking on
     const JTok *tk = W.tok + H.tok0;
@@ -391,7 +555,7 @@ __device__ __forceinline__ void kj_piece(const DecompressArgs &A, const JWork &W
             for (uint32_t k = 0; k < 16; k++) pt[k] = x + k;
         } else {
             const uint32_t D = t.kd & ~kJCopy;
-            for (uint32_t k = 0; k < 16; k++) pt[k] = p0 + k >= D ? x + k - D : kJZero;
+            for (uint32_t k = 0; k < 16; k++) pt[k] = p0 + k + hb >= D ? x + k - D : kJZero;
         }
         return;
     }
@@ -411,14 +575,15 @@ __device__ __forceinline__ void kj_piece(const DecompressArgs &A, const JWork &W
             pt[k] = x;
         } else {
             const uint32_t D = t.kd & ~kJCopy;
-            pt[k] = p >= D ? x - D : kJZero;
+            pt[k] = p + hb >= D ? x - D : kJZero;
         }
         by[k >> 2] |= v << (8 * (k & 3));
     }
 }
 
 __global__ __launch_bounds__(256) void kj_expand(DecompressArgs A, JWork W) {
-    const uint64_t ob = A.out_off[0], g0 = ob & ~15ull, end = A.out_off[A.count];
+    const uint64_t ob = A.out_off[0], g0 = jg0(A), end = A.out_off[A.count];
+    const uint64_t hst = A.c_on ? ob - A.c_hist : ob;  // (c_on) the history [hst, ob): final bytes, pointing at themselves
     for (uint64_t g = g0 + ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 16; g < end; g += (uint64_t)gridDim.x * blockDim.x * 16) {
         // the stream of the piece's first byte of the batch (binary search over the slots)
         const uint64_t x0 = g > ob ? g : ob;
@@ -442,6 +607,7 @@ __global__ __launch_bounds__(256) void kj_expand(DecompressArgs A, JWork W) {
         }
         // a piece at a slot's end (or before the batch's first slot): each stream's output bytes in it,
         // byte by byte
+        for (uint64_t y = g > hst ? g : hst; y < ob && y < ge; y++) W.ptr[y - g0] = (uint32_t)(y - g0);
         for (uint64_t x = x0; x < ge;) {
             while (s + 1 < (uint32_t)A.count && A.out_off[s + 1] <= x) s++;
             const JHead Hs = W.head[s];
@@ -463,23 +629,25 @@ __global__ __launch_bounds__(256) void kj_expand(DecompressArgs A, JWork W) {
 // ---- 4: one pointer-jumping pass (returns at once when the pass before changed nothing)
 __global__ __launch_bounds__(256) void kj_jump(DecompressArgs A, JWork W, int pass) {
     if (pass > 0 && W.pass[pass - 1] == 0) return;
-    const uint64_t end = A.out_off[A.count] - (A.out_off[0] & ~15ull);  // (ptr counts from g0)
+    const uint64_t end = A.out_off[A.count] - jg0(A);  // (ptr counts from g0)
     bool changed = false;
     for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; g < end; g += (uint64_t)gridDim.x * blockDim.x * 4) {
         uint4 v = g + 4 <= end ? *(const uint4 *)(W.ptr + g) : make_uint4(kJGap, kJGap, kJGap, kJGap);
         if (g + 4 > end)
             for (uint64_t k = g; k < end; k++) (&v.x)[k - g] = W.ptr[k];
         uint32_t *e = &v.x;
-        bool any = false;
+        // the four gathers issued together (a pointer to itself or a marker is final)
+        uint32_t r[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t q = e[k];
-            if (q >= kJZero || q == (uint32_t)(g + k)) continue;
-            const uint32_t r = W.ptr[q];
-            if (r != q) {
-                e[k] = r;
-                any = true;
-            }
+            r[k] = q >= kJZero || q == (uint32_t)(g + k) ? q : W.ptr[q];
+        }
+        bool any = false;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            any |= r[k] != e[k];
+            e[k] = r[k];
         }
         if (any) {
             changed = true;
@@ -493,7 +661,7 @@ __global__ __launch_bounds__(256) void kj_jump(DecompressArgs A, JWork W, int pa
 
 // ---- 5a: every copied byte from its resolved source
 __global__ __launch_bounds__(256) void kj_gather(DecompressArgs A, JWork W) {
-    const uint64_t g0 = A.out_off[0] & ~15ull, end = A.out_off[A.count] - g0;
+    const uint64_t g0 = jg0(A), end = A.out_off[A.count] - g0;
     uint8_t *o = A.out + g0;
     for (uint64_t g = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; g < end; g += (uint64_t)gridDim.x * blockDim.x * 4) {
         for (uint64_t x = g; x < g + 4 && x < end; x++) {
@@ -504,8 +672,16 @@ __global__ __launch_bounds__(256) void kj_gather(DecompressArgs A, JWork W) {
     }
 }
 
-// ---- 5b: results, or the stream to the exact decoder
+// ---- 5b: results, or the stream to the exact decoder; a one-stream batch's Break positions from
+// (chunk, local position) to the stream's output positions
 __global__ __launch_bounds__(256) void kj_final(DecompressArgs A, JWork W) {
+    if (A.breaks && A.count == 1 && blockIdx.x == 0 && !W.head[0].state) {
+        const uint64_t nbrk = A.breaks[0] < A.breaks_cap ? A.breaks[0] : A.breaks_cap;
+        for (uint64_t k = threadIdx.x; k < nbrk; k += blockDim.x) {
+            const uint64_t v = A.breaks[1 + k];
+            A.breaks[1 + k] = W.cobase[v >> 32] + (v & 0xffffffffull);
+        }
+    }
     for (uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; s < A.count; s += (uint64_t)gridDim.x * blockDim.x) {
         const JHead H = W.head[s];
         if (H.state) {
@@ -518,6 +694,11 @@ __global__ __launch_bounds__(256) void kj_final(DecompressArgs A, JWork W) {
         if (A.end_state) {  // (one MetaReset, before any output: r.pos is the output since the start)
             A.end_state[0] = H.bsl < 0 ? 0 : (int64_t)1 << H.bsl;
             A.end_state[1] = (int64_t)H.total;
+            if (A.c_on) {
+                A.end_state[2] = H.tstop;
+                A.end_state[3] = H.tj;
+                A.end_state[4] = H.tL;
+            }
         }
     }
 }
@@ -527,10 +708,10 @@ size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 // the workspace layout of a batch (in_total / out_total: the end offsets in_off[count], out_off[count])
 struct JLayout {
     uint64_t chunks, tok_cap;
-    size_t o_head, o_cbase, o_entry, o_sexit, o_bits, o_cnt, o_cout, o_cflag, o_ctb, o_cob, o_tok, o_ptr, o_pass, total;
+    size_t o_head, o_cbase, o_entry, o_sexit, o_bits, o_cnt, o_cout, o_cflag, o_ctb, o_cob, o_tok, o_ltok, o_maxd, o_ptr, o_pass, total;
     JLayout(uint64_t count, uint64_t in_total, uint64_t out_total) {
         chunks = in_total / kJC + 2 * count + 2;
-        tok_cap = in_total + 16;
+        tok_cap = in_total / 2 + chunks + 16;  // (a token takes >= 2 input bytes; one may start in each chunk's last byte)
         size_t off = 0;
         auto take = [&](size_t n) {
             const size_t o = off;
@@ -539,7 +720,8 @@ struct JLayout {
         };
         o_head = take(sizeof(JHead) * count), o_cbase = take(4 * (count + 1)), o_entry = take(4 * chunks), o_sexit = take(4 * chunks),
         o_bits = take(4 * kJW * chunks), o_cnt = take(4 * chunks), o_cout = take(8 * chunks), o_cflag = take(4 * chunks),
-        o_ctb = take(8 * chunks), o_cob = take(8 * chunks), o_tok = take(sizeof(JTok) * tok_cap), o_ptr = take(4 * out_total + 16),
+        o_ctb = take(8 * chunks), o_cob = take(8 * chunks), o_tok = take(sizeof(JTok) * tok_cap),
+        o_ltok = take(sizeof(JTok) * kJRec * chunks), o_maxd = take(4 * chunks), o_ptr = take(4 * out_total + 16),
         o_pass = take(8 * (kJPasses + 2));
         total = off;
     }
@@ -583,7 +765,7 @@ hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
     uint64_t in_total = 0, out_bytes = 0;
     hipError_t e = batch_extents(a, st, &in_total, &out_bytes);
     if (e != hipSuccess) return e;
-    const uint64_t out_total = out_bytes + 16;
+    const uint64_t out_total = out_bytes + (a.c_on ? a.c_hist : 0) + 16;  // (+ the history a continuation reads)
     const JLayout Y(a.count, in_total, out_total);
     const uint64_t chunks = Y.chunks, tok_cap = Y.tok_cap;
     const size_t o_head = Y.o_head, o_cbase = Y.o_cbase, o_entry = Y.o_entry, o_sexit = Y.o_sexit, o_bits = Y.o_bits, o_cnt = Y.o_cnt,
@@ -613,6 +795,8 @@ hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
     W.cobase = (uint64_t *)(w + o_cob);
     W.tok = (JTok *)(w + o_tok);
     W.tok_cap = tok_cap;
+    W.ltok = (JTok *)(w + Y.o_ltok);
+    W.cmaxd = (uint32_t *)(w + Y.o_maxd);
     W.ptr = (uint32_t *)(w + o_ptr);
     W.pass = (uint32_t *)(w + o_pass);
     uint64_t *tok_alloc = (uint64_t *)(W.pass + kJPasses + 2);
@@ -621,16 +805,21 @@ hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
     hipLaunchKernelGGL(kj_init, dim3(1), dim3(1024), 0, st, a, W);
     const unsigned cgrid = (unsigned)((chunks + 63) / 64);
     hipLaunchKernelGGL(kj_spec, dim3(cgrid), dim3(64), 0, st, a, W);
-    hipLaunchKernelGGL(kj_prop, dim3((unsigned)a.count), dim3(64), 0, st, a, W);
-    hipLaunchKernelGGL(kj_count, dim3(cgrid), dim3(64), 0, st, a, W);
+    hipLaunchKernelGGL(kj_verify, dim3(cgrid), dim3(64), 0, st, a, W);
+    hipLaunchKernelGGL(kj_fix, dim3((unsigned)a.count), dim3(64), 0, st, a, W);
+    hipLaunchKernelGGL(kj_tok, dim3(cgrid), dim3(64), 0, st, a, W);
     hipLaunchKernelGGL(kj_scan, dim3((unsigned)a.count), dim3(64), 0, st, a, W, tok_alloc);
-    hipLaunchKernelGGL(kj_emit, dim3(cgrid), dim3(64), 0, st, a, W);
+    hipLaunchKernelGGL(kj_place, dim3((unsigned)chunks), dim3(64), 0, st, a, W);
     const uint64_t pieces = (out_total + 15) / 16;  // (out_total: the batch's output and the alignment slack)
     const unsigned egrid = (unsigned)(pieces / 256 + 1 < 8192 ? pieces / 256 + 1 : 8192);
     hipLaunchKernelGGL(kj_expand, dim3(egrid), dim3(256), 0, st, a, W);
     const uint64_t quads = (out_total + 3) / 4;
     const unsigned jgrid = (unsigned)(quads / 256 + 1 < 8192 ? quads / 256 + 1 : 8192);
-    for (int k = 0; k < kJPasses; k++) hipLaunchKernelGGL(kj_jump, dim3(jgrid), dim3(256), 0, st, a, W, k);
+    // every pass at least halves the longest pointer chain, and a chain is shorter than the output:
+    // ceil(log2(output)) + 1 passes finish it (the ones after it return at once)
+    int passes = 1;
+    while (passes < kJPasses && ((uint64_t)1 << (passes - 1)) < out_total) passes++;
+    for (int k = 0; k < passes; k++) hipLaunchKernelGGL(kj_jump, dim3(jgrid), dim3(256), 0, st, a, W, k);
     hipLaunchKernelGGL(kj_gather, dim3(jgrid), dim3(256), 0, st, a, W);
     hipLaunchKernelGGL(kj_final, dim3((unsigned)((a.count + 255) / 256)), dim3(256), 0, st, a, W);
     return hipGetLastError();

@@ -100,7 +100,7 @@ __host__ __device__ __forceinline__ V16 win16(V16 a, V16 b, uint32_t o) {
 }
 
 #ifndef __HIP_DEVICE_COMPILE__
-inline uint64_t g_ring_iters = 0;
+inline uint64_t g_ring_iters = 0, g_ring_stat[8] = {0, 0, 0, 0, 0, 0, 0, 0};  // (host emulation statistics)
 #endif
 
 // decodes stream s with `ring` (kRing + 16 bytes, with 16-byte guards on both sides) as its history; false = hand
@@ -276,6 +276,15 @@ __host__ __device__ __forceinline__ bool ring_one(const DecompressArgs &A, const
         rp += kk;
         rem -= kk;
         if (pair) ring_st(ring, dst, hv);  // the paired literal at the output position (dst == pos)
+#ifndef __HIP_DEVICE_COMPILE__
+        if (live) {
+            g_ring_stat[0]++;
+            if (!np) g_ring_stat[src == 0 ? 1 : (src == 1 ? 2 : 3)]++;  // a long token's inner move: HBM / pattern / ring
+            if (np && pair) g_ring_stat[4]++;
+            if (np && !pair && !cp) g_ring_stat[5]++;  // a literal parsed alone
+            if (np && !pair && cp) g_ring_stat[6]++;   // a copy parsed alone
+        }
+#endif
         dst = pair ? dst + L1 : dst;
         pos = pair ? pos + L1 : pos;
         // ---- the next token's state (a padding or meta step has L = 0: no move)

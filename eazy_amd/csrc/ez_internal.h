@@ -127,6 +127,17 @@ struct DecompressArgs {
     // batch: host hints, in_off[count] - in_off[0] and out_off[count] - out_off[0] (0 = unknown: the
     // K2j route and its workspace then read the offsets back, which waits for the stream)
     uint64_t in_bytes, out_bytes;
+    // K2j, one stream (count == 1) continuing a Reader's stream (ez_reader_read's read-ahead, c_on):
+    // the input is what the Reader has buffered, so it may end inside a token (the chain stops before
+    // it); c_bsl: the window's log2 at the input's start (-1: none yet); c_hist: bytes of the window's
+    // history right before out + out_off[0] (the last min(r.pos, len(r.block)) decoded bytes);
+    // c_pos0: r.pos there (a MetaReset then hands the stream over unless c_pos0 and the output before
+    // it are 0).  end_state then gets {window bytes, output bytes, input consumed by whole tokens, and
+    // for a literal starting there whose body runs past the input its header length and length}
+    int c_on;
+    int32_t c_bsl;
+    uint64_t c_hist;
+    int64_t c_pos0;
 };
 
 // words of workspace the two-level batch decoder needs
@@ -148,6 +159,9 @@ uint64_t long_scratch_bytes(const CompressArgs &a);
 hipError_t launch_long(const CompressArgs &a, uint8_t *recs, hipStream_t s);
 // K1L on a Writer handle's single Write (the handle's ring as history, its table in and out)
 bool long_ring_applies(const CompressArgs &a);
+// Writes up to this many bytes K1L stages in LDS (the input read once): the handle path then lets the
+// kernels read the Write from, and write the output to, pinned host memory (no copies)
+constexpr uint64_t kHandleLdsWrite = 49152;
 uint64_t long_ring_scratch_bytes(const CompressArgs &a);
 hipError_t launch_long_ring(const CompressArgs &a, uint8_t *recs, hipStream_t s);
 bool compress_forced_general();  // ez_select_compress_kernel('w') (tests, A/B)

@@ -27,12 +27,18 @@ struct K2Tok {
 
 enum { kParseSkip = 0, kParseToken = 1, kParseHandOver = -1 };
 enum { kScanReset = 2 };  // k2_scan only: a MetaReset, valid only before any output
+// k2_scan with partial (a Reader's buffered input, which may end inside a token): the step at i runs
+// past the input's end.  t.adv = 0: its header (or meta) is incomplete, nothing of it is consumed
+// (readTag / continueMetaTag return ErrShortBuffer at i, reader.go:218-325); else a literal whose
+// header is whole and whose body runs past the end (read copies the bytes there are, :166-168)
+enum { kScanTail = 3 };
 
 // The checks that do not depend on the decoder's state, for a step at input position
 // i: returns kParseSkip (padding, break, version, magic), kScanReset, kParseToken or
 // kParseHandOver.  h = input bytes i .. i+15 (zeros past the batch); nb = stream
 // bytes; lim32 = BlockSizeLimit clamped to 32 bits (0x7fffffff: none), limit = the 64-bit one
-__host__ __device__ __forceinline__ int k2_scan(V16 h, int32_t i, int32_t nb, int32_t lim32, int64_t limit, K2Tok &t) {
+__host__ __device__ __forceinline__ int k2_scan(V16 h, int32_t i, int32_t nb, int32_t lim32, int64_t limit, K2Tok &t,
+                                                bool partial = false) {
     const uint64_t lo = h.lo;
     const uint32_t t0 = (uint32_t)lo & 0xff, l7 = t0 & 0x7f;
     t.L = 0;
@@ -42,6 +48,7 @@ __host__ __device__ __forceinline__ int k2_scan(V16 h, int32_t i, int32_t nb, in
     t.marg = 0;
     if (t0 == 0) {  // padding, a run of zero bytes at once
         t.adv = lo ? (int32_t)(__builtin_ctzll(lo) >> 3) : (h.hi ? 8 + (int32_t)(__builtin_ctzll(h.hi) >> 3) : 16);
+        if (partial && i + t.adv > nb) t.adv = nb - i;  // (readTag skips the zeros up to the input's end)
         return kParseSkip;
     }
     if (t0 == 0x80) {
@@ -53,6 +60,10 @@ __host__ __device__ __forceinline__ int k2_scan(V16 h, int32_t i, int32_t nb, in
         const bool m_rst = mt == kMetaReset && mln == 1 && marg <= 32 && (limit == 0 || (1ll << marg) <= limit);
         const bool m_ver = mt == kMetaVer && mln == 1 && marg == 0;
         const bool m_mag = mt == kMetaMagic && mln == 4 && (uint32_t)(lo >> 16) == 0x797a6165u;
+        if (partial && ml != 6 && i + 2 + mln > nb) {
+            t.adv = 0;
+            return kScanTail;
+        }
         if (ml == 6 || i + 2 + mln > nb || !(m_brk || m_rst || m_ver || m_mag)) return kParseHandOver;
         t.adv = 2 + mln;
         t.marg = marg;
@@ -79,9 +90,20 @@ __host__ __device__ __forceinline__ int k2_scan(V16 h, int32_t i, int32_t nb, in
     const uint32_t k = 1 + on;
     const uint32_t D = lng ? (uint32_t)D0 : (uint32_t)D0 + (uint32_t)L;  // < 2^32
     const int32_t adv = cp ? (int32_t)(jo + k) : (int32_t)j + L;
+    if (partial && (uint32_t)i + (cp ? (uint32_t)adv : j) > (uint32_t)nb) {  // the header runs past the input
+        t.adv = 0;
+        return kScanTail;
+    }
+    const bool past = (uint32_t)i + (uint32_t)adv > (uint32_t)nb;
     const bool bad = l7 == 127 || (l7 == 126 && lx >= (1u << 30)) || (cp && o >= 254 && (o == 255 || ox >= (1u << 30))) || L > lim32 ||
-                     (uint32_t)i + (uint32_t)adv > (uint32_t)nb || (cp && D >= (1u << 30));
+                     (past && !partial) || (cp && D >= (1u << 30));
     if (bad) return kParseHandOver;
+    if (past) {  // (partial) a literal whose body runs past the input
+        t.adv = adv;
+        t.L = L;
+        t.j = (int32_t)j;
+        return kScanTail;
+    }
     t.adv = adv;
     t.L = L;
     t.j = (int32_t)j;

@@ -159,6 +159,15 @@ int ez_reader_pending(const ez_reader *r); /* r.state != 0 (reader.go:135) */
 int ez_reader_set_whole(ez_reader *r, int whole);
 /* 1 when this stream's Reads are being served from the whole-stream decode (tests, measurement). */
 int ez_reader_whole_decoded(const ez_reader *r);
+/* NewReader(io.Reader) handles (set_whole 0) read ahead: a Read with nothing decoded ahead and at
+ * least 8 KiB of buffered input b[i..b_len) decodes every whole token of it at once on the device
+ * (K2j continuing the stream from the handle's state, a literal the buffer ends inside of decoded as
+ * far as it goes), and the Reads are served from that output -- the same bytes, ErrBreak and errors at
+ * the same Reads as Read by Read, and ErrShortBuffer (the shim's refill, more()) with *i_out where
+ * Read by Read would ask for more input.  A buffer the device path hands over (an error, a MetaReset
+ * after output, ...) is decoded Read by Read until more input arrives.  The number of read-aheads
+ * this handle has made (tests, measurement): */
+int64_t ez_reader_ahead_count(const ez_reader *r);
 
 /* ---- device-resident batches of independent streams (the GPU hot path) ----
  * One stream = a fresh NewWriter(block, htable) receiving one Write; its

@@ -629,6 +629,83 @@ static int perf_reader(const char *comp_path, const char *plain_path, size_t rs,
     return ok ? 0 : 1;
 }
 
+// --perf-stream COMP PLAIN READ PIECE: NewReader over an io.Reader that returns PIECE bytes per call
+// (the README's usage, reader.go:79-86), read to EOF with Read(READ bytes) through the C++ mirror;
+// checked against PLAIN; prints the rate and the handle's read-ahead count
+static int perf_stream(const char *comp_path, const char *plain_path, size_t rs, size_t piece) {
+    const std::vector<uint8_t> comp = read_file(comp_path), plain = read_file(plain_path);
+    std::vector<uint8_t> got(plain.size() + rs), p(rs);
+    {  // (once per process: the HIP runtime's start and the device's decode workspace)
+        Chunked warm;
+        warm.b = comp;
+        warm.step = piece;
+        auto w = NewReader(&warm);
+        for (int k = 0; k < 64; k++) (void)w->Read(p.data(), rs);
+    }
+    Chunked src;
+    src.b = comp;
+    src.step = piece;
+    const auto t0 = std::chrono::steady_clock::now();
+    auto r = NewReader(&src);
+    size_t at = 0;
+    Err e = Err::OK;
+    for (;;) {
+        auto [n, err] = r->Read(p.data(), rs);
+        if (at + n > got.size()) return 3;
+        std::memcpy(got.data() + at, p.data(), n);
+        at += n;
+        e = err;
+        if (err != Err::OK) break;
+    }
+    const double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    const bool ok = e == Err::EOF_ && at == plain.size() && std::memcmp(got.data(), plain.data(), at) == 0;
+    std::printf("{\"reader\": \"stream\", \"read_bytes\": %zu, \"piece\": %zu, \"MiBps\": %.1f, \"read_aheads\": %lld, \"ok\": %s}\n", rs,
+                piece, (double)at / t / 1048576.0, (long long)ez_reader_ahead_count(r->Handle()), ok ? "true" : "false");
+    return ok ? 0 : 1;
+}
+
+// --reader-ahead: a 3 MiB log-like stream written by the mirror's Writer, read back through
+// NewReader(io.Reader) in 64 KiB pieces with Read(4096) and in 9,000-byte pieces with Read(777): the
+// bytes equal the input and the handle read ahead
+static int reader_ahead_test() {
+    Bytes plain;
+    uint32_t x = 12345;
+    const char *words[] = {"GET /api/v1/items ", "status=200 ", "user=alice ", "latency_ms=", "trace=", "INFO ", "WARN ", "\n"};
+    while (plain.size() < (3u << 20)) {
+        x = x * 1103515245u + 12345u;
+        const char *wd = words[(x >> 16) % 8];
+        plain.insert(plain.end(), wd, wd + std::strlen(wd));
+        const std::string num = std::to_string((x >> 8) % 100000);
+        plain.insert(plain.end(), num.begin(), num.end());
+    }
+    Buffer buf;
+    auto w = NewWriter(&buf, MiB, 1024);
+    for (size_t at = 0; at < plain.size(); at += 65536) {
+        const size_t n = std::min((size_t)65536, plain.size() - at);
+        auto [k, err] = w->Write(plain.data() + at, n);
+        if (err != Err::OK || k != n) return 2;
+    }
+    for (auto [piece, rs] : {std::pair<size_t, size_t>{65536, 4096}, {9000, 777}}) {
+        Chunked src;
+        src.b = buf.b;
+        src.step = piece;
+        auto r = NewReader(&src);
+        Bytes got, p(rs);
+        Err e = Err::OK;
+        for (;;) {
+            auto [n, err] = r->Read(p.data(), rs);
+            got.insert(got.end(), p.begin(), p.begin() + (ptrdiff_t)n);
+            e = err;
+            if (err != Err::OK) break;
+        }
+        const long long ra = (long long)ez_reader_ahead_count(r->Handle());
+        std::printf("piece %zu read %zu: %zu bytes, %s, read-aheads %lld\n", piece, rs, got.size(), ez_strerror((int)e), ra);
+        if (e != Err::EOF_ || got != plain || ra <= 0) return 1;
+    }
+    std::printf("ok\n");
+    return 0;
+}
+
 // Dumper::ReadFrom with the stream in one read prints what one Write prints, and a stream cut
 // inside a token ends in UnexpectedEOF (reader.go:563-600).  (Reads that cut a token do not
 // print what Dump prints: like the reference, Write reports the bytes up to the cut token's
@@ -675,6 +752,8 @@ static void TestDumperReadFrom() {
 int main(int argc, char **argv) {
     if (argc > 2 && std::string(argv[1]) == "--dump") return dump_file(argv[2]);
     if (argc > 5 && std::string(argv[1]) == "--perf-reader") return perf_reader(argv[2], argv[3], (size_t)std::atol(argv[4]), std::atoi(argv[5]));
+    if (argc > 5 && std::string(argv[1]) == "--perf-stream") return perf_stream(argv[2], argv[3], (size_t)std::atol(argv[4]), (size_t)std::atol(argv[5]));
+    if (argc > 1 && std::string(argv[1]) == "--reader-ahead") return reader_ahead_test();
     const bool cpu = argc > 1 && std::string(argv[1]) == "--cpu";
     run("TestPrintLengthEncoding", TestPrintLengthEncoding);
     run("TestPrintOffsetEncoding", TestPrintOffsetEncoding);

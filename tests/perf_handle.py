@@ -96,13 +96,24 @@ def main():
         assert bytes(got) == b"".join(ws)
         res[str(size)]["reader_4k_MiBps"] = len(got) / t_r / 2**20
     # Reader.Read(4 KiB) loop over a 16 MiB stream: NewReaderBytes (whole-stream decode on the first Read,
-    # ez_reader_set_whole) against the same handle decoding Read by Read (set_whole 0, NewReader's mode)
+    # ez_reader_set_whole) and NewReader over an io.Reader returning 64 KiB pieces (the README's usage:
+    # each refill read ahead on the device)
     plain = src[: 16 << 20]
     comp = orc.compress(1 << 20, 1024, [plain[k : k + 65536] for k in range(0, len(plain), 65536)])
     rd = {}
-    for mode, whole in (("whole", 1), ("read_by_read", 0)):
-        r = ez.NewReaderBytes(comp)
-        L.ez_reader_set_whole(r._h, whole)
+
+    class Pieces:
+        def __init__(self, b, piece):
+            self.b, self.at, self.piece = b, 0, piece
+
+        def read_go(self, k):
+            m = min(k, self.piece, len(self.b) - self.at)
+            d = self.b[self.at : self.at + m]
+            self.at += m
+            return d, (ez.EOF if self.at == len(self.b) else ez.OK)
+
+    for mode in ("whole", "stream_64k"):
+        r = ez.NewReaderBytes(comp) if mode == "whole" else ez.NewReader(Pieces(comp, 65536))
         got = bytearray()
         t0 = time.perf_counter()
         t1 = None
@@ -114,9 +125,11 @@ def main():
                 break
             assert err == ez.OK
         t_r = time.perf_counter() - t0
-        assert bytes(got) == plain and r.whole_decoded == bool(whole)
+        assert bytes(got) == plain
         rd[mode + "_MiBps"] = len(plain) / t_r / 2**20
         rd[mode + "_first_read_ms"] = (t1 - t0) * 1e3
+        if mode == "stream_64k":
+            rd["stream_64k_read_aheads"] = r.ahead_count
     t0 = time.perf_counter()
     assert orc.decompress(comp, 4096)[0] == plain
     rd["cpu_oracle_read4k_MiBps"] = len(plain) / (time.perf_counter() - t0) / 2**20
@@ -131,13 +144,20 @@ def main():
             cf, pf = os.path.join(d, "c.bin"), os.path.join(d, "p.bin")
             open(cf, "wb").write(comp)
             open(pf, "wb").write(plain)
-            for whole in (1, 0):
-                p = subprocess.run([exe, "--perf-reader", cf, pf, "4096", str(whole)], capture_output=True, text=True, timeout=300)
-                line = [x for x in p.stdout.splitlines() if x.startswith("{")]
-                if p.returncode == 0 and line:
-                    j = json.loads(line[0])
-                    rd[f"cpp_{j['reader']}_MiBps"] = j["MiBps"]
-                    rd[f"cpp_{j['reader']}_first_read_ms"] = j["first_read_ms"]
+            p = subprocess.run([exe, "--perf-reader", cf, pf, "4096", "1"], capture_output=True, text=True, timeout=300)
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+            if p.returncode == 0 and line:
+                j = json.loads(line[0])
+                rd["cpp_whole_MiBps"] = j["MiBps"]
+                rd["cpp_whole_first_read_ms"] = j["first_read_ms"]
+            p = subprocess.run([exe, "--perf-stream", cf, pf, "4096", "65536"], capture_output=True, text=True, timeout=300)
+            line = [x for x in p.stdout.splitlines() if x.startswith("{")]
+            if p.returncode == 0 and line:
+                j = json.loads(line[0])
+                rd["cpp_stream_64k_MiBps"] = j["MiBps"]
+                rd["cpp_stream_64k_read_aheads"] = j["read_aheads"]
+            else:
+                rd["cpp_stream_64k_error"] = (p.stdout + p.stderr)[-300:]
     print(json.dumps({"handle_path": res, "writes_per_size": a.writes, "reader_16MiB_read4k": rd,
                       "note": "ez_writer_write per call: one pinned H2D copy, the general kernel (a wave), one D2H copy, one sync; "
                               "batch64: ez_writer_write_batch of 64 Writes per call"}))
