@@ -15,6 +15,7 @@
 #include <vector>
 #include <memory>
 #include <thread>
+#include <chrono>
 
 #include "ez_cache.h"
 #include "ez_format.h"
@@ -229,13 +230,14 @@ extern "C" size_t ez_compress_bound(size_t n) { return (size_t)ez::compress_boun
 struct HBuf {
     void *p = nullptr;
     size_t cap = 0;
+    unsigned flags = hipHostMallocDefault;  // (a Writer's: coherent, the kernels read and write it in place)
     int ensure(size_t n) {
         if (n <= cap) return EZ_OK;
         if (p) (void)hipHostFree(p);
         p = nullptr;
         cap = 0;
         size_t c = n < 65536 ? 65536 : n + n / 4;
-        if (hipHostMalloc(&p, c, hipHostMallocDefault) != hipSuccess) return EZ_EDEVICE;
+        if (hipHostMalloc(&p, c, flags) != hipSuccess) return EZ_EDEVICE;
         cap = c;
         return EZ_OK;
     }
@@ -265,6 +267,7 @@ struct ez_writer {
     HBuf host;             // the same layout, pinned
     uint8_t *host_dev = nullptr;  // the device's address of `host` (zero-copy Writes), or nullptr
     void *host_alias_of = nullptr;  // the host.p host_dev was taken for
+    uint32_t seq = 0;               // the zero-copy path's completion flag value of the last Write
     hipStream_t stream = nullptr;
 };
 
@@ -300,6 +303,7 @@ extern "C" int ez_writer_new(int64_t block, int64_t htable, int device, ez_write
     if (!g.ok) return EZ_EDEVICE;
     ez_writer *w = new ez_writer();
     w->device = device;
+    w->host.flags = hipHostMallocCoherent;
     if (hipStreamCreateWithFlags(&w->stream, hipStreamNonBlocking) != hipSuccess) {
         delete w;
         return EZ_EDEVICE;
@@ -397,7 +401,8 @@ int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t
     // [input | per Write: in_off[2] out_off[2] out_size status | outputs, Write j's at its bound prefix]
     const size_t o_meta = (n + 15) & ~(size_t)15;
     const size_t o_o = (o_meta + 6 * 8 * k + 15) & ~(size_t)15;
-    const size_t total = o_o + bound + 16;
+    const size_t o_flag = (o_o + bound + 16 + 63) & ~(size_t)63;  // the completion flag (zero-copy path)
+    const size_t total = o_flag + 64;
     // Writes K1L stages in LDS (read once): the kernels read them, and write the output, in the pinned
     // host buffer itself -- no host->device and device->host copies (a 100-byte Write's fixed cost)
     bool zc = true;
@@ -433,13 +438,28 @@ int writer_run_long(ez_writer *w, const uint8_t *p, const uint64_t *ends, size_t
     if (!zc) EZ_HIP(hipMemcpyAsync(D, H, o_meta + 6 * 8 * k, hipMemcpyHostToDevice, w->stream));
     w->tainted = true;  // (cleared when the call completes, or by the reset of a failed one)
     hipError_t he = hipSuccess;
+    volatile uint32_t *flag = (volatile uint32_t *)(H + o_flag);
+    const uint32_t seq = ++w->seq;
+    *flag = seq + 1;  // (not the value this call waits for, whatever the buffer held)
     for (size_t j = 0; j < k && he == hipSuccess; j++) {
         const uint64_t len = ends[j] - (j ? ends[j - 1] : 0);
-        const ez::CompressArgs a = long_args(w, D, (uint64_t *)(D + o_meta) + 6 * j, j, len, w->pos + (int64_t)(j ? ends[j - 1] : 0));
+        ez::CompressArgs a = long_args(w, D, (uint64_t *)(D + o_meta) + 6 * j, j, len, w->pos + (int64_t)(j ? ends[j - 1] : 0));
+        if (zc && j + 1 == k) {  // the last Write's kernel signals its end in the pinned buffer
+            a.done_flag = (uint32_t *)(D + o_flag);
+            a.done_seq = seq;
+        }
         he = ez::launch_long_ring(a, w->recs.as<uint8_t>(), w->stream);
     }
     if (he == hipSuccess && !zc) he = hipMemcpyAsync(H + o_meta, D + o_meta, o_o - o_meta + bound, hipMemcpyDeviceToHost, w->stream);
-    if (he == hipSuccess) he = hipStreamSynchronize(w->stream);
+    bool seen = false;
+    if (he == hipSuccess && zc) {
+        // wait by polling the flag (a few microseconds sooner than the runtime's synchronisation); a
+        // kernel that does not signal within 100 ms is waited for, and its error reported, by the runtime
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t spin = 0; !(seen = *flag == seq); spin++)
+            if ((spin & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(100)) break;
+    }
+    if (he == hipSuccess && !seen) he = hipStreamSynchronize(w->stream);
     if (he != hipSuccess) {
         (void)writer_zero(w);
         return EZ_EDEVICE;

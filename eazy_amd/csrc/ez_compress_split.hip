@@ -2213,6 +2213,17 @@ __global__ __launch_bounds__(256) void kc_v2(CompressArgs A, KcBufs B, int pass)
 // ones clamped: the far skip, writer.go:219-221, still sees them as far), the history before the Write
 // from the handle's ring (RingSrc).  The table goes back to the handle, converted back, at the end.
 constexpr int32_t kRelFar = 1 << 28;  // |relative position| clamp (bs <= 2^26, Writes < 2^27 bytes)
+template <bool WIDE>
+__device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
+                                            uint64_t *stage = nullptr);
+// the staged ring bytes for a Write of n bytes: 16 n, at least kRingMin, at most kLdsRing
+#ifndef EZ_K1R_RL
+#define EZ_K1R_RL 32768
+#endif
+__device__ __forceinline__ int32_t knob_dev_rl(int32_t n) {
+    const int32_t r = 16 * n < EZ_K1R_RL ? EZ_K1R_RL : (16 * n > kLdsRing ? kLdsRing : ((16 * n + 15) & ~15));
+    return r > kLdsRing ? kLdsRing : r;
+}
 template <bool LDS>
 __global__ __launch_bounds__(256) void k1_long_ring(CompressArgs A, uint4 *recs, uint64_t rcap) {
     constexpr int G = 16;
@@ -2224,7 +2235,12 @@ __global__ __launch_bounds__(256) void k1_long_ring(CompressArgs A, uint4 *recs,
     const uint8_t *p = A.in + A.in_off[0];
     const int32_t n = (int32_t)(A.in_off[1] - A.in_off[0]);
     uint8_t *lds = smem + (size_t)A.hs * 4;
-    const int32_t rl = A.bs < kLdsRing ? (int32_t)A.bs : kLdsRing;
+    // the ring's last rl bytes staged before the Write (older candidates read the ring in HBM; staging
+    // less for small Writes measured no faster: 100-byte Writes 26.2 / 27.2 against 26.8 / 25.2 us at
+    // 4 KiB and 32 KiB, two alternating runs; -DEZ_K1R_RL=<bytes> builds for A/B)
+    static_assert(kLdsRing % 16 == 0, "");
+    const int32_t want = knob_dev_rl(n);
+    const int32_t rl = A.bs < want ? (int32_t)A.bs : want;
     const uint32_t mask = (uint32_t)(A.bs - 1);
     if (LDS) {  // the ring's last rl bytes, the Write, 64 zeros: 16 bytes per lane and step, 4 loads in flight
         const RingSrc R{p, p, p + n, A.ring, A.start, mask};
@@ -2280,6 +2296,19 @@ __global__ __launch_bounds__(256) void k1_long_ring(CompressArgs A, uint4 *recs,
         }
     }
     if (tid == 0) A.out_size[0] = (uint64_t)nrec | ((uint64_t)err << 48);
+    if (LDS) {
+        // the token writer (k1_emit's emit_stream) by wave 0 of the same block: one launch per Write
+        __threadfence();
+        __syncthreads();
+        if (tid < 64) emit_stream<true>(A, (const uint64_t *)recs, rcap, 0, lane);
+        if (A.done_flag) {
+            __syncthreads();
+            if (tid == 0) {
+                __threadfence_system();
+                __hip_atomic_store(A.done_flag, A.done_seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+    }
 }
 
 // the Write's last min(n, bs) bytes into the handle's ring (block[(start + k) & mask], copyData)
@@ -2297,9 +2326,6 @@ __global__ __launch_bounds__(256) void k1_ring_store(CompressArgs A) {
 // launcher).  A live stream (n >= 4) lacks the 64 bytes before or the 64 after it only if it starts
 // in the batch's first 64 bytes (at most 16 such streams, each >= 4 bytes) or ends in its last 64
 // (at most 16): 32 slots always suffice.
-template <bool WIDE>
-__device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
-                                            uint64_t *stage = nullptr);
 
 // waves per SIMD the VGPR budget is cut for: 8-lane groups are held to ~2 by their tables' LDS, so
 // they keep VGPRs (no spills); (EZ_EXP & 8192 builds: 16-lane groups at 4, A/B)
@@ -3288,12 +3314,14 @@ hipError_t launch_long_ring(const CompressArgs &a, uint8_t *recs, hipStream_t st
         (void)hipFuncSetAttribute((const void *)k1_long_ring<true>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
         attr_done = true;
     }
-    // Writes of up to kLdsWrite bytes: the Write and the ring's last bytes in LDS
-    if (a.max_len <= (uint64_t)kLdsWrite)
+    // Writes of up to kLdsWrite bytes: the Write and the ring's last bytes in LDS, the token writer in
+    // the same kernel
+    if (a.max_len <= (uint64_t)kLdsWrite) {
         hipLaunchKernelGGL(k1_long_ring<true>, dim3(1), dim3(256), (size_t)a.hs * 4 + kLdsRing + kLdsWrite + 64, st, a, (uint4 *)recs,
                            rcap);
-    else
-        hipLaunchKernelGGL(k1_long_ring<false>, dim3(1), dim3(256), (size_t)a.hs * 4, st, a, (uint4 *)recs, rcap);
+        return hipGetLastError();
+    }
+    hipLaunchKernelGGL(k1_long_ring<false>, dim3(1), dim3(256), (size_t)a.hs * 4, st, a, (uint4 *)recs, rcap);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k1_emit<true>, dim3(1), dim3(256), 0, st, a, (const uint64_t *)recs, rcap);

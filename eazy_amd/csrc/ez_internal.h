@@ -73,6 +73,10 @@ struct CompressArgs {
     uint32_t *spec_nlit;
     uint32_t win_bytes;       // general kernel, long streams: LDS window bytes (set by its launcher)
     int no_k1c;               // K1c's workspace could not be had: K1L alone (set by the C-ABI's retry)
+    // a Writer handle's Write on K1L's LDS path: when set, the kernel's last act is storing done_seq
+    // there (pinned host memory, system scope) so that the caller can wait by polling it
+    uint32_t *done_flag;
+    uint32_t done_seq;
 };
 
 
