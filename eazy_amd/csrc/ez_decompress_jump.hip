@@ -6,32 +6,41 @@
 // handle's one stream, C4's 64 buckets, 1 MiB streams) to a handful of waves on a 1,024-SIMD chip.
 // K2j cuts both chains into data-parallel steps:
 //
-//  1. token starts (kj_spec, kj_prop): the compressed stream is cut into 2 KiB chunks; a lane per
-//     chunk parses speculatively from the chunk's first byte and records the positions it visits
-//     (a bitmap) and where it leaves the chunk.  A wrong start parses garbage, but its chain meets
-//     the true one within a few tokens (median ~110 bytes on the log streams; 99 % within 1 KiB),
-//     after which both are the same chain.  One wave per stream then carries the true entry
-//     through the chunks 64 at a time: lane j takes chunk j's entry to be chunk j-1's speculative
-//     exit and walks the true chain from it until it meets a recorded position (the chunks agree)
-//     or leaves the chunk (the first lane that does ends the step with the true exit it walked);
-//     an entry past a chunk (inside a long token) skips to the chunk it lies in.
-//  2. tokens (kj_count, kj_scan, kj_emit): a lane per chunk walks the true chain from its entry,
-//     counts tokens and output bytes, and checks every form (k2_scan, ez_k2_parse.h); a wave per
-//     stream scans the chunks' counts into token and output positions and validates the stream
-//     as K2t does (one MetaReset before any output, the window set before the first token, every
-//     distance within the window, the output within the slot); the lanes then write one record
-//     per token (output position, length, distance or input position).
+//  1. token starts (kj_spec, kj_verify, kj_fix): the compressed stream is cut into 1 KiB chunks; a
+//     lane per chunk parses speculatively from kJWarm bytes before the chunk and records the
+//     positions it visits inside it (a bitmap) and where it leaves it.  A wrong start parses
+//     garbage, but its chain meets the true one within a few tokens (median ~110 bytes on the log
+//     streams; 99 % within 1 KiB), after which both are the same chain, so the warm-up has usually
+//     met it before the chunk starts.  kj_verify (a lane per chunk, all in parallel) takes chunk j's
+//     entry to be chunk j-1's speculative exit and walks the true chain from it until it meets a
+//     recorded position (the chunk's exit is then the speculative one) or leaves the chunk.
+//     kj_fix (a wave per stream) finds, 64 chunks per step, the first chunk whose assumed entry
+//     differs from its predecessor's true exit and re-walks only that chunk (rare); an entry past a
+//     chunk (inside a long token) skips to the chunk it lies in.
+//  2. tokens (kj_tok, kj_scan, kj_place): a lane per chunk walks the true chain from its entry
+//     once, checks every form (k2_scan, ez_k2_parse.h) and writes a chunk-local record per token
+//     (output position from the chunk's start, length, distance or input position), its token and
+//     output counts, the longest distance and its Breaks; a wave per stream scans the chunks'
+//     counts into token and output positions and validates the stream as K2t does (one MetaReset
+//     before any output, the window set before the first token, every distance within the window,
+//     the output within the slot); kj_place moves each chunk's records into the stream's array.
 //  3. bytes (kj_expand): a thread per 16 output bytes finds its tokens (a binary search over the
 //     stream's records), writes literal bytes and zero regions, and for every copied byte p a
 //     pointer ptr[p] = p - D (a marker for bytes before the stream start: the fresh window's zeros,
-//     SURVEY A.12); literal and zero bytes point at themselves.
+//     SURVEY A.12; a Reader's continuation points into the history placed before out_off[0]);
+//     literal, zero and history bytes point at themselves.
 //  4. copies (kj_jump): pointer jumping, ptr[p] = ptr[ptr[p]] over all bytes, until every pointer
 //     names a literal byte, a zero byte or the zero marker: ceil(log2(chain depth)) passes, each a
 //     sequential read and a gather that stays mostly local (copy distances are short).  Passes
 //     after the one that changed nothing return at once (the launcher queues a fixed number, so
 //     nothing waits on the host).
 //  5. kj_gather writes every copied byte from its resolved source; kj_final reports each stream
-//     (out_size, status, a Reader's end state) or hands it to the exact decoder.
+//     (out_size, status, Break positions, a Reader's end state) or hands it to the exact decoder.
+//
+// Continuation (DecompressArgs.c_on, a NewReader's read-ahead, ez_capi.hip stream_ahead): one stream
+// whose history (c_hist bytes) sits before out_off[0]; the chain stops before a token the input ends
+// inside of, a literal whose body runs past the input is output as far as it goes, and the end state
+// says where the input was left.
 //
 // Streams K2j cannot take as a whole (an error, a form k2_scan hands over, a MetaReset after output,
 // a slot too small) go to the exact decoder (ez_decompress.hip), which recomputes them from the start.
@@ -118,7 +127,7 @@ __device__ __forceinline__ int32_t jadv(const uint8_t *b, int32_t p, int32_t nb,
     return r == kParseHandOver ? -1 : t.adv;
 }
 
-// The walks of kj_spec / kj_count / kj_emit read their chunk's tokens from LDS: a block's 64 chunks are
+// The walks of kj_spec / kj_verify / kj_tok read their chunk's tokens from LDS: a block's 64 chunks are
 // consecutive in the batch's input (a stream's chunks follow each other, and so do the streams), so
 // the block stages the bytes from its first chunk's start to 16 past its last chunk's end with
 // coalesced 16-byte loads, and every token step is then an LDS read instead of a dependent global
@@ -172,9 +181,9 @@ __device__ __forceinline__ int32_t jadv_s(const JStage &S, uint64_t b0, int32_t 
 }
 
 // The input bytes the token (or padding run, or meta) at the 16 bytes h takes, for the speculative
-// walks (kj_spec, kj_prop): the same advance as k2_scan for every form it accepts, from 32-bit
+// walks (kj_spec, kj_verify, kj_fix): the same advance as k2_scan for every form it accepts, from 32-bit
 // arithmetic on the header's first 8 bytes and no checks (a form k2_scan hands over advances by some
-// amount >= 1 here; kj_count's full parse of the true chain then hands the stream over)
+// amount >= 1 here; kj_tok's full parse of the true chain then hands the stream over)
 __device__ __forceinline__ int32_t jadv_fast(V16 h) {
     const uint32_t w0 = (uint32_t)h.lo, w1 = (uint32_t)(h.lo >> 32);
     const uint32_t t0 = w0 & 0xff, l7 = t0 & 0x7f;
@@ -321,7 +330,7 @@ __global__ __launch_bounds__(64) void kj_verify(DecompressArgs A, JWork W) {
         if (x < 0) x = q;
     }
     W.entry[c] = (uint32_t)a;
-    W.cnt[c] = (uint32_t)x;  // (the true exit; kj_count overwrites cnt with the token count)
+    W.cnt[c] = (uint32_t)x;  // (the true exit; kj_tok overwrites cnt with the token count)
 }
 
 __global__ __launch_bounds__(64) void kj_fix(DecompressArgs A, JWork W) {
@@ -378,7 +387,7 @@ __global__ __launch_bounds__(64) void kj_fix(DecompressArgs A, JWork W) {
         k = kw + 1;
     }
     // the chain must end exactly at the stream's end (else the last token runs past the input; a
-    // Reader's read-ahead, c_on, stops before that token: kj_count finds it)
+    // Reader's read-ahead, c_on, stops before that token: kj_tok finds it)
     const int32_t last = nch - 1 == fx_at ? fx_val : (int32_t)texit[c00 + nch - 1];
     if (lane == 0 && (A.c_on ? last < nb : last != nb)) H.state = 1;
 }

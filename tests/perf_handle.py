@@ -159,7 +159,8 @@ def main():
             else:
                 rd["cpp_stream_64k_error"] = (p.stdout + p.stderr)[-300:]
     print(json.dumps({"handle_path": res, "writes_per_size": a.writes, "reader_16MiB_read4k": rd,
-                      "note": "ez_writer_write per call: one pinned H2D copy, the general kernel (a wave), one D2H copy, one sync; "
+                      "note": "ez_writer_write per call (Writes up to 48 KiB): one launch of K1L with the token writer fused, "
+                              "input and output in the handle's coherent pinned buffer, completion by polling a flag; "
                               "batch64: ez_writer_write_batch of 64 Writes per call"}))
 
 

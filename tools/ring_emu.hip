@@ -43,6 +43,10 @@ int main(int argc, char **argv) {
         if (!(hw ? ez::ring_one<true>(a, s, ring + 16) : ez::ring_one<false>(a, s, ring + 16))) size[s] = ~0ull;  // front guard
 #ifndef __HIP_DEVICE_COMPILE__
     std::fprintf(stderr, "iterations per stream %.1f\n", (double)ez::g_ring_iters / (double)(count ? count : 1));
+    const double c = (double)(count ? count : 1);
+    std::fprintf(stderr, "per stream: live steps %.1f, inner moves HBM %.1f pattern %.1f ring %.1f; pairs %.1f, lone literals %.1f, lone copies %.1f\n",
+                 ez::g_ring_stat[0] / c, ez::g_ring_stat[1] / c, ez::g_ring_stat[2] / c, ez::g_ring_stat[3] / c, ez::g_ring_stat[4] / c,
+                 ez::g_ring_stat[5] / c, ez::g_ring_stat[6] / c);
 #endif
     FILE *fo = std::fopen(argv[4], "wb");
     for (uint64_t s = 0; s < count; s++)
