@@ -43,8 +43,6 @@ namespace {
 
 constexpr int64_t kChunk = 16384;     // positions per kx_pred chunk (chunk-local distances fit u16)
 constexpr uint32_t kNone = 0xffffffffu;
-constexpr int64_t kPiece = 256;       // kx_judge: positions per block step
-static_assert(kChunk % kPiece == 0, "kx_judge reads one kx_pred chunk's table per piece");
 constexpr int64_t kCopyPiece = 65536; // kx_copy: bytes per block step
 constexpr int kRounds = 8;            // rounds before the general kernel takes the rest (EZ_K1X_ROUNDS)
 // A stream whose accepted position lay within kDenseGap bytes of the round's start in kDenseRounds
@@ -222,12 +220,14 @@ __device__ __forceinline__ V16 ld16_al(const uint8_t *y, const uint8_t *lo, cons
 // vx = stream bytes x-8 .. x+7.  Positions in 32 bits (K1x takes streams under 2 GiB): the
 // judgement is most of K1x's time and every 64-bit compare or min is two instructions; only the
 // window size bs stays 64-bit
+// CL(y) gives stream bytes y .. y+15 (y >= -8; kx_judge: from its LDS window when staged)
+template <class CL>
 __device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t *p, int32_t n, int32_t x, int32_t cand, int32_t done,
-                                           const V16 vx, const uint8_t *lo, const uint8_t *hi) {
+                                           const V16 vx, const CL &cl16) {
     const int64_t bs = A.bs;
     if (cand >= done && x > cand) {
         // off >= 0 and i > done + off: writeRunlen with st = cand (writer.go:227-231, 441-473)
-        const V16 vc = ld16_al(p + cand - 8, lo, hi);
+        const V16 vc = cl16(cand - 8);
         if (cand + 8 < n && vc.hi == 0) return true;  // writeZeros: >= 8 zeros at st
         const uint64_t df = vx.hi ^ vc.hi, db = vx.lo ^ vc.lo;
         int32_t f = df ? (int32_t)(__builtin_ctzll(df) >> 3) : 8;
@@ -242,7 +242,7 @@ __device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t 
     // holds stream byte done - bs + ((y - done) & mask), zero before the stream
     V16 vc;
     if (cand - 8 >= 0 && (int64_t)cand - 8 >= (int64_t)done - bs && cand + 8 <= done) {
-        vc = ld16_al(p + cand - 8, lo, hi);
+        vc = cl16(cand - 8);
     } else {
         vc = V16{0, 0};
         const int64_t mask = bs - 1;
@@ -266,63 +266,100 @@ __device__ __forceinline__ bool kx_accepts(const CompressArgs &A, const uint8_t 
     return len >= kMinCopyChunk;
 }
 
-// blocks step over (piece j, active stream a), pieces of 256 positions from `from` on, so the
-// early pieces of every active stream are judged first and a stream's later pieces are skipped
-// once an accepted position before them is known
+// Blocks step over (segment j, active stream a): segments of kSeg positions from `from` on (one
+// kx_pred chunk each), in steps of 256 positions, so the early segments of every active stream are
+// judged first and the rest of a stream's segment is skipped once an accepted position before its
+// step is known.  The block stages the segment's bytes and the kBack bytes before it in LDS by
+// coalesced 16-byte loads: a candidate is the nearest earlier same-hash position (C4's fp32 buckets:
+// ~1 KiB back with 1,024 hashes), so nearly every candidate's 16 bytes come from LDS instead of a
+// gather that missed the CU's caches (the staged bytes of that piece were another block's); a
+// candidate farther back is loaded from the batch.
+constexpr int32_t kSeg = (int32_t)kChunk;  // positions per block task
+constexpr int32_t kBack = 8192;            // history bytes staged before the segment
+constexpr int32_t kStageWords = (kBack + kSeg + 48) / 4;
+static_assert(kStageWords % 4 == 0, "the stage is loaded in 16-byte pieces");
 __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
-    __shared__ uint32_t S[kPiece / 4 + 8];  // the piece's bytes x-8 .. x+23 for its 256 positions, as aligned words
+    extern __shared__ __attribute__((aligned(16))) uint32_t S[];  // kStageWords: bytes [xs - kBack - 8, xs + kSeg + 40), aligned
     __shared__ bool skip;
     const uint64_t nact = B.nact[0];
-    const uint64_t kp = (A.max_len + kPiece - 1) / kPiece + 1;
+    const uint64_t ks = (A.max_len + kSeg - 1) / kSeg + 1;
     const uint32_t hsh = hshift(A.hs);
     const int lane = (int)(threadIdx.x & 63);
     const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
-    for (uint64_t q = blockIdx.x; q < nact * kp; q += gridDim.x) {
+    for (uint64_t q = blockIdx.x; q < nact * ks; q += gridDim.x) {
         const uint64_t j = q / nact, s = B.act[q % nact];
         const SpecState sp = A.spec[s];
         const int32_t n = (int32_t)slen(A, s), from = (int32_t)sp.from, done = (int32_t)sp.done;  // (< 2 GiB)
-        const int32_t xb = (from & ~(kPiece - 1)) + (int32_t)j * kPiece;
-        if (xb + 4 > n) continue;  // uniform: the block's values only
+        const int32_t xs = (from & ~(kSeg - 1)) + (int32_t)j * kSeg;
+        if (xs + 4 > n) continue;  // uniform: the block's values only
         const uint8_t *p = A.in + A.in_off[s];
-        // the piece's rows, block-uniform (a piece never straddles a kx_pred chunk: both aligned)
         const uint16_t *prow = B.pred + s * A.max_len;
-        const uint32_t *trow = B.tabs + (s * B.kmax + (uint64_t)(xb / kChunk)) * (uint64_t)A.hs;
+        const uint32_t *trow = B.tabs + (s * B.kmax + (uint64_t)(xs / kChunk)) * (uint64_t)A.hs;
         const uint32_t *srow = A.spec_tab + s * (uint64_t)A.hs;
-        // stage bytes [xb - 8, xb + kPiece + 24) by coalesced aligned words (outside the batch: 0);
-        // whether an accept before the piece is known already is read once, by thread 0 (another
-        // block's atomicMin may land between two threads' reads: the decision must be the block's)
-        const uint8_t *wa = (const uint8_t *)((uintptr_t)(p + xb - 8) & ~(uintptr_t)3);
-        const uint32_t r0 = (uint32_t)((uintptr_t)(p + xb - 8) & 3);
-        __syncthreads();  // the previous piece's readers are done
-        if (threadIdx.x == 0) skip = (int64_t)xb > (int64_t)__atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
-        if (threadIdx.x < kPiece / 4 + 8) {
-            const uint8_t *w = wa + 4 * threadIdx.x;
-            uint32_t v = 0;
-            if (w >= lo && w + 4 <= hi) v = *(const uint32_t *)w;
-            else
-                for (int t = 0; t < 4; t++)
-                    if (w + t >= lo && w + t < hi) v |= (uint32_t)w[t] << (8 * t);
-            S[threadIdx.x] = v;
-        }
+        // the stage: aligned words from floor4(p + xs - kBack - 8), bytes outside the batch 0
+        const int32_t base = xs - kBack - 8;  // stream offset of the stage's first byte (less r0)
+        const uint8_t *wa = (const uint8_t *)((uintptr_t)(p + base) & ~(uintptr_t)3);
+        const int32_t r0 = (int32_t)((uintptr_t)(p + base) & 3);
+        __syncthreads();  // the previous task's readers are done
+        if (threadIdx.x == 0) skip = (int64_t)xs > (int64_t)__atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
         __syncthreads();
         if (skip) continue;
-        const int32_t x = xb + (int32_t)threadIdx.x;
-        bool acc = false;
-        if (x >= from && x + 4 <= n) {
-            const uint32_t o = r0 + threadIdx.x, k = o >> 2, r = o & 3;
-            const uint32_t d0 = S[k], d1 = S[k + 1], d2 = S[k + 2], d3 = S[k + 3], d4 = S[k + 4];
-            const V16 vx{(uint64_t)__builtin_amdgcn_alignbyte(d1, d0, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32),
-                         (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, r) << 32)};
-            const uint32_t h = ((uint32_t)vx.hi * kHashMul) >> hsh;
-            const uint16_t d = prow[x];
-            // nearest earlier same-hash position (chunk-local, else the chunk's incoming entry);
-            // before `from` the table at `from` holds the entry
-            const int32_t pc = d ? x - d : (int32_t)trow[h];
-            const int32_t cand = pc >= from ? pc : (int32_t)srow[h];
-            acc = kx_accepts(A, p, n, x, cand, done, vx, lo, hi);
+        for (int32_t k = 4 * (int32_t)threadIdx.x; k < kStageWords; k += 4 * 256) {
+            const uint8_t *w = wa + 4 * k;
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (w >= lo && w + 16 <= hi) {
+                v = *(const uint4 *)w;
+            } else {
+                uint32_t d[4] = {0, 0, 0, 0};
+                for (int t = 0; t < 16; t++)
+                    if (w + t >= lo && w + t < hi) d[t >> 2] |= (uint32_t)w[t] << (8 * (t & 3));
+                v = make_uint4(d[0], d[1], d[2], d[3]);
+            }
+            *(uint4 *)(S + k) = v;
         }
-        const uint64_t m = wballot(acc);
-        if (m && lane == ffs64(m)) atomicMin(&B.first[s], (uint32_t)x);
+        __syncthreads();
+        // bytes y .. y+15 of the stream: staged when y >= base, else from the batch
+        auto cl16 = [&](int32_t y) -> V16 {
+            if (y >= base) {
+                const uint32_t o = (uint32_t)(y - base + r0), kq = o >> 2, r = o & 3;
+                const uint32_t d0 = S[kq], d1 = S[kq + 1], d2 = S[kq + 2], d3 = S[kq + 3], d4 = S[kq + 4];
+                return V16{(uint64_t)__builtin_amdgcn_alignbyte(d1, d0, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32),
+                           (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, r) << 32)};
+            }
+            return ld16_al(p + y, lo, hi);
+        };
+        // The steps: no barrier among them (the stage is read-only now), each wave decides alone
+        // whether an accepted position before its step is known (a wave that skips a step only
+        // skips positions after an accepted one, so the first accepted position stays exact, stale
+        // reads included).  The next step's kx_pred distances and the first accepted position are
+        // loaded one step ahead, so no step waits for a load issued in it.
+        const int32_t xe = xs + kSeg < n - 3 ? xs + kSeg : n - 3;  // positions x with x + 4 <= n
+        int32_t xb = xs;
+        uint32_t fa = __atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
+        uint16_t d = xb + (int32_t)threadIdx.x < xe ? prow[xb + (int32_t)threadIdx.x] : (uint16_t)0;
+        for (; xb < xe; xb += 256) {
+            if ((int64_t)xb > (int64_t)fa) break;  // (wave-uniform)
+            const int32_t x = xb + (int32_t)threadIdx.x;
+            const uint16_t dn = x + 256 < xe ? prow[x + 256] : (uint16_t)0;
+            const uint32_t fn = __atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
+            bool acc = false;
+            if (x >= from && x < xe) {
+                const uint32_t o = (uint32_t)(x - 8 - base + r0), kq = o >> 2, r = o & 3;
+                const uint32_t d0 = S[kq], d1 = S[kq + 1], d2 = S[kq + 2], d3 = S[kq + 3], d4 = S[kq + 4];
+                const V16 vx{(uint64_t)__builtin_amdgcn_alignbyte(d1, d0, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d2, d1, r) << 32),
+                             (uint64_t)__builtin_amdgcn_alignbyte(d3, d2, r) | ((uint64_t)__builtin_amdgcn_alignbyte(d4, d3, r) << 32)};
+                const uint32_t h = ((uint32_t)vx.hi * kHashMul) >> hsh;
+                // nearest earlier same-hash position (chunk-local, else the chunk's incoming entry);
+                // before `from` the table at `from` holds the entry
+                const int32_t pc = d ? x - d : (int32_t)trow[h];
+                const int32_t cand = pc >= from ? pc : (int32_t)srow[h];
+                acc = kx_accepts(A, p, n, x, cand, done, vx, cl16);
+            }
+            const uint64_t m = wballot(acc);
+            if (m && lane == ffs64(m)) atomicMin(&B.first[s], (uint32_t)x);
+            d = dn;
+            fa = fn;
+        }
     }
 }
 
@@ -449,12 +486,17 @@ hipError_t launch_compress_spec(const CompressArgs &a0, uint8_t *scratch, hipStr
     if (!check()) return e;
     hipLaunchKernelGGL(kx_scan, dim3((unsigned)((a.count * (uint64_t)a.hs + 255) / 256)), dim3(256), 0, st, a, B);
     if (!check()) return e;
-    const unsigned jgrid = 2048;  // 8 blocks of 4 waves per CU
+    const unsigned jgrid = 2048;  // 8 blocks of 4 waves per CU (kx_judge: as many as its LDS stage lets fit)
+    static bool jattr = false;
+    if (!jattr) {
+        (void)hipFuncSetAttribute((const void *)kx_judge, hipFuncAttributeMaxDynamicSharedMemorySize, kStageWords * 4);
+        jattr = true;
+    }
     static const uint32_t dense_rounds = (uint32_t)knob("EZ_K1X_DENSE", (int)kDenseRounds);  // (0: never, A/B)
     for (int r = 0; r < rounds(); r++) {
         hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B, dense_rounds);
         if (!check()) return e;
-        hipLaunchKernelGGL(kx_judge, dim3(jgrid), dim3(256), 0, st, a, B);
+        hipLaunchKernelGGL(kx_judge, dim3(jgrid), dim3(256), (size_t)kStageWords * 4, st, a, B);
         if (!check()) return e;
         hipLaunchKernelGGL(kx_merge, dim3(count), dim3(256), 2 * tlds, st, a, B);
         if (!check()) return e;
