@@ -100,9 +100,20 @@ __global__ __launch_bounds__(64) void kx_init(CompressArgs A, KxBufs B) {
     A.spec[s] = SpecState{0u, 0u, (uint32_t)h.n, 0u};
 }
 
-// chunk (s, k): block s * kmax + k, one wave
+// chunk (s, k): block s * kmax + k, one wave.  The chunk's bytes pass through a 4 KiB LDS ring in
+// 1 KiB pieces (one 16-byte load per lane), each loaded two pieces ahead, so the positions'
+// sequential lane-ordered exchanges read their 4 bytes from LDS and no step waits for a load.
+constexpr int32_t kPredPiece = 1024;
+constexpr int32_t kPredRing = 4 * kPredPiece;
+__device__ __forceinline__ uint4 kx_ld16z(const uint8_t *w, const uint8_t *blo, const uint8_t *bhi) {
+    if (w >= blo && w + 16 <= bhi) return *(const uint4 *)w;
+    uint32_t d[4] = {0, 0, 0, 0};
+    for (int u = 0; u < 16; u++)
+        if (w + u >= blo && w + u < bhi) d[u >> 2] |= (uint32_t)w[u] << (8 * (u & 3));
+    return make_uint4(d[0], d[1], d[2], d[3]);
+}
 __global__ __launch_bounds__(64) void kx_pred(CompressArgs A, KxBufs B) {
-    extern __shared__ uint32_t T[];
+    extern __shared__ __attribute__((aligned(16))) uint32_t T[];  // hs entries, then the ring
     const uint64_t s = blockIdx.x / B.kmax, k = blockIdx.x % B.kmax;
     const int lane = (int)threadIdx.x;
     const int64_t n = slen(A, s);
@@ -111,20 +122,38 @@ __global__ __launch_bounds__(64) void kx_pred(CompressArgs A, KxBufs B) {
     const uint8_t *p = A.in + A.in_off[s];
     uint16_t *pr = B.pred + s * A.max_len;  // per stream: a refused over-long stream cannot shift the others
     const uint32_t hsh = hshift(A.hs);
-    for (int64_t h = lane; h < A.hs; h += 64) T[h] = kNone;
-    __syncthreads();
+    uint32_t *R = T + A.hs;
+    const uint8_t *blo = A.in, *bhi = A.in + A.in_off[A.count];
+    const uint8_t *wa = (const uint8_t *)((uintptr_t)(p + lo) & ~(uintptr_t)3);
+    const uint32_t r0 = (uint32_t)((uintptr_t)(p + lo) & 3);
     const int64_t hi = lo + kChunk < n - 3 ? lo + kChunk : n - 3;  // hashed positions: x + 4 <= n
-    for (int64_t b = lo; b < hi; b += 64) {
-        const int64_t x = b + lane;
-        if (x < hi) {
-            const uint32_t h = hash4(p + x, hsh);
-            // lane-ordered exchange: the previous value is the nearest earlier position of the
-            // chunk with this hash (an earlier lane of this step, or an earlier step)
-            const uint32_t prev = atomicExch(&T[h], (uint32_t)x);
-            pr[x] = prev == kNone ? (uint16_t)0 : (uint16_t)(x - (int64_t)prev);
+    // pieces of the stage, from floor4(p + lo): piece c holds its bytes [c * 1 KiB, +1 KiB)
+    const int32_t np = (int32_t)((hi - lo + r0 + 3 + kPredPiece - 1) / kPredPiece);
+    const uint4 v0 = kx_ld16z(wa + 16 * lane, blo, bhi);
+    const uint4 v1 = np > 1 ? kx_ld16z(wa + kPredPiece + 16 * lane, blo, bhi) : make_uint4(0, 0, 0, 0);
+    for (int64_t h = lane; h < A.hs; h += 64) T[h] = kNone;
+    *(uint4 *)(R + 4 * lane) = v0;
+    *(uint4 *)(R + kPredPiece / 4 + 4 * lane) = v1;
+    for (int32_t c = 0; c < np; c++) {
+        // piece c + 2 into registers now, into the ring after this piece's steps (its slot held c - 2)
+        const bool more = c + 2 < np;
+        const uint4 vn = more ? kx_ld16z(wa + (int64_t)(c + 2) * kPredPiece + 16 * lane, blo, bhi) : make_uint4(0, 0, 0, 0);
+        // positions whose first byte lies in piece c
+        const int64_t xa = lo + (int64_t)c * kPredPiece - r0, xz = xa + kPredPiece < hi ? xa + kPredPiece : hi;
+        for (int64_t b = xa > lo ? xa : lo; b < xz; b += 64) {
+            const int64_t x = b + lane;
+            if (x < xz) {
+                const uint32_t o = (uint32_t)(x - lo) + r0, kq = o >> 2, r = o & 3;
+                const uint32_t w0 = R[kq & (kPredRing / 4 - 1)], w1 = R[(kq + 1) & (kPredRing / 4 - 1)];
+                const uint32_t h = (__builtin_amdgcn_alignbyte(w1, w0, r) * kHashMul) >> hsh;
+                // lane-ordered exchange: the previous value is the nearest earlier position of the
+                // chunk with this hash (an earlier lane of this step, or an earlier step)
+                const uint32_t prev = atomicExch(&T[h], (uint32_t)x);
+                pr[x] = prev == kNone ? (uint16_t)0 : (uint16_t)(x - (int64_t)prev);
+            }
         }
+        if (more) *(uint4 *)(R + ((c + 2) & 3) * (kPredPiece / 4) + 4 * lane) = vn;
     }
-    __syncthreads();
     uint32_t *tab = B.tabs + (uint64_t)blockIdx.x * (uint64_t)A.hs;
     for (int64_t h = lane; h < A.hs; h += 64) tab[h] = T[h];
 }
@@ -325,6 +354,9 @@ __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
             }
             *(uint4 *)(S + k) = v;
         }
+        // the chunk's incoming entries (a position whose hash has no earlier one in the chunk)
+        uint32_t *T = S + kStageWords;
+        for (int32_t h = (int32_t)threadIdx.x; h < (int32_t)A.hs; h += 256) T[h] = trow[h];
         __syncthreads();
         // bytes y .. y+15 of the stream: staged when y >= base, else from the batch
         auto cl16 = [&](int32_t y) -> V16 {
@@ -337,19 +369,17 @@ __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
             return ld16_al(p + y, lo, hi);
         };
         // The steps: no barrier among them (the stage is read-only now), each wave decides alone
-        // whether an accepted position before its step is known (a wave that skips a step only
-        // skips positions after an accepted one, so the first accepted position stays exact, stale
-        // reads included).  The next step's kx_pred distances and the first accepted position are
-        // loaded one step ahead, so no step waits for a load issued in it.
+        // whether an accepted position before its steps is known (a wave that skips steps only skips
+        // positions after an accepted one, so the first accepted position stays exact, stale reads
+        // included).  Four steps of 256 positions per group; the next group's kx_pred distances and
+        // the first accepted position are loaded at the top of a group, four steps before their use.
         const int32_t xe = xs + kSeg < n - 3 ? xs + kSeg : n - 3;  // positions x with x + 4 <= n
+        const int32_t tid = (int32_t)threadIdx.x;
+        auto ldd = [&](int32_t x) -> uint32_t { return x < xe ? (uint32_t)prow[x] : 0u; };
         int32_t xb = xs;
         uint32_t fa = __atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
-        uint16_t d = xb + (int32_t)threadIdx.x < xe ? prow[xb + (int32_t)threadIdx.x] : (uint16_t)0;
-        for (; xb < xe; xb += 256) {
-            if ((int64_t)xb > (int64_t)fa) break;  // (wave-uniform)
-            const int32_t x = xb + (int32_t)threadIdx.x;
-            const uint16_t dn = x + 256 < xe ? prow[x + 256] : (uint16_t)0;
-            const uint32_t fn = __atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
+        uint32_t dA = ldd(xb + tid), dB = ldd(xb + 256 + tid), dC = ldd(xb + 512 + tid), dD = ldd(xb + 768 + tid);
+        auto step = [&](int32_t x, uint32_t d) {
             bool acc = false;
             if (x >= from && x < xe) {
                 const uint32_t o = (uint32_t)(x - 8 - base + r0), kq = o >> 2, r = o & 3;
@@ -359,13 +389,26 @@ __global__ __launch_bounds__(256) void kx_judge(CompressArgs A, KxBufs B) {
                 const uint32_t h = ((uint32_t)vx.hi * kHashMul) >> hsh;
                 // nearest earlier same-hash position (chunk-local, else the chunk's incoming entry);
                 // before `from` the table at `from` holds the entry
-                const int32_t pc = d ? x - d : (int32_t)trow[h];
+                const int32_t pc = d ? x - (int32_t)d : (int32_t)T[h];
                 const int32_t cand = pc >= from ? pc : (int32_t)srow[h];
                 acc = kx_accepts(A, p, n, x, cand, done, vx, cl16);
             }
             const uint64_t m = wballot(acc);
             if (m && lane == ffs64(m)) atomicMin(&B.first[s], (uint32_t)x);
-            d = dn;
+        };
+        for (; xb < xe; xb += 1024) {
+            if ((int64_t)xb > (int64_t)fa) break;  // (wave-uniform)
+            const int32_t xn = xb + 1024 + tid;
+            const uint32_t nA = ldd(xn), nB = ldd(xn + 256), nC = ldd(xn + 512), nD = ldd(xn + 768);
+            const uint32_t fn = __atomic_load_n(&B.first[s], __ATOMIC_RELAXED);
+            step(xb + tid, dA);
+            if (xb + 256 < xe) step(xb + 256 + tid, dB);
+            if (xb + 512 < xe) step(xb + 512 + tid, dC);
+            if (xb + 768 < xe) step(xb + 768 + tid, dD);
+            dA = nA;
+            dB = nB;
+            dC = nC;
+            dD = nD;
             fa = fn;
         }
     }
@@ -488,23 +531,28 @@ hipError_t launch_compress_spec(const CompressArgs &a0, uint8_t *scratch, hipStr
     const unsigned count = (unsigned)a.count;
     const unsigned chunks = (unsigned)(a.count * B.kmax);
     const size_t tlds = (size_t)a.hs * 4;
+    static bool pattr = false;
+    if (!pattr) {
+        (void)hipFuncSetAttribute((const void *)kx_pred, hipFuncAttributeMaxDynamicSharedMemorySize, 4096 * 4 + kPredRing);
+        pattr = true;
+    }
     hipLaunchKernelGGL(kx_init, dim3(count), dim3(64), 0, st, a, B);
     if (!check()) return e;
-    hipLaunchKernelGGL(kx_pred, dim3(chunks), dim3(64), tlds, st, a, B);
+    hipLaunchKernelGGL(kx_pred, dim3(chunks), dim3(64), tlds + (size_t)kPredRing, st, a, B);
     if (!check()) return e;
     hipLaunchKernelGGL(kx_scan, dim3((unsigned)((a.count * (uint64_t)a.hs + 255) / 256)), dim3(256), 0, st, a, B);
     if (!check()) return e;
     const unsigned jgrid = 2048;  // 8 blocks of 4 waves per CU (kx_judge: as many as its LDS stage lets fit)
     static bool jattr = false;
     if (!jattr) {
-        (void)hipFuncSetAttribute((const void *)kx_judge, hipFuncAttributeMaxDynamicSharedMemorySize, kStageWords * 4);
+        (void)hipFuncSetAttribute((const void *)kx_judge, hipFuncAttributeMaxDynamicSharedMemorySize, (kStageWords + 4096) * 4);
         jattr = true;
     }
     static const uint32_t dense_rounds = (uint32_t)knob("EZ_K1X_DENSE", (int)kDenseRounds);  // (0: never, A/B)
     for (int r = 0; r < rounds(); r++) {
         hipLaunchKernelGGL(kx_reset, dim3(1), dim3(1024), 0, st, a, B, dense_rounds);
         if (!check()) return e;
-        hipLaunchKernelGGL(kx_judge, dim3(jgrid), dim3(256), (size_t)kStageWords * 4, st, a, B);
+        hipLaunchKernelGGL(kx_judge, dim3(jgrid), dim3(256), (size_t)(kStageWords + a.hs) * 4, st, a, B);
         if (!check()) return e;
         hipLaunchKernelGGL(kx_merge, dim3(count), dim3(256), 2 * tlds, st, a, B);
         if (!check()) return e;
