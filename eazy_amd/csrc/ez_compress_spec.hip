@@ -166,10 +166,24 @@ __global__ __launch_bounds__(256) void kx_scan(CompressArgs A, KxBufs B) {
     const int64_t n = slen(A, s);
     const uint64_t kn = n > 3 ? (uint64_t)((n - 3 + kChunk - 1) / kChunk) : 0;
     uint32_t run = 0;
-    for (uint64_t k = 0; k < kn && k < B.kmax; k++) {
-        uint32_t *e = B.tabs + (s * B.kmax + k) * (uint64_t)A.hs + h;
-        const uint32_t v = *e;
-        *e = run;
+    const uint64_t ke = kn < B.kmax ? kn : B.kmax;
+    uint32_t *e = B.tabs + (s * B.kmax) * (uint64_t)A.hs + h;
+    const uint64_t st = (uint64_t)A.hs;
+    uint64_t k = 0;
+    // eight chunks' entries loaded before any is rewritten (the loads do not wait for each other)
+    for (; k + 8 <= ke; k += 8) {
+        uint32_t v[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) v[t] = e[(k + t) * st];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+            e[(k + t) * st] = run;
+            if (v[t] != kNone) run = v[t];
+        }
+    }
+    for (; k < ke; k++) {
+        const uint32_t v = e[k * st];
+        e[k * st] = run;
         if (v != kNone) run = v;
     }
 }
