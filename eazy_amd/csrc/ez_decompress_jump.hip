@@ -54,7 +54,7 @@
 namespace ez {
 namespace {
 
-constexpr int32_t kJC = 1024;                        // compressed bytes per chunk
+constexpr int32_t kJC = 1024;                        // compressed bytes per chunk at most (JWork.jc: 1,024 or 256)
 constexpr int32_t kJW = kJC / 32;                    // bitmap words per chunk
 constexpr uint32_t kJGap = 0xffffffffu;              // ptr: not a byte of any stream's output
 constexpr uint32_t kJZero = 0xfffffffeu;             // ptr: a zero byte of the history before the stream
@@ -98,7 +98,15 @@ struct JWork {
     uint32_t *cmaxd;    // the longest copy distance of a chunk
     uint32_t *ptr;
     uint32_t *pass;     // [kJPasses]: the pass changed something; [kJPasses]: token records allocated
+    int32_t jc;         // compressed bytes per chunk (jchunk)
 };
+
+// Chunks of 256 bytes for batches of at most 96 KiB of input (a Reader's refill of ~64 KiB: four
+// times the lanes, each walk a quarter as long -- one wave of 1 KiB chunks was the refill's critical
+// path: 0.60 -> 0.51 ms; C++ NewReader over 64 KiB pieces 143 -> 200 - 208 MiB/s), 1 KiB above (at
+// 122 / 244 KiB, 256-byte chunks measured 0.85 / 1.03 against 0.82 / 0.66 ms: the per-stream scan and
+// fix over four times the chunks outweigh the shorter walks)
+inline int32_t jchunk(uint64_t in_total) { return in_total <= (96ull << 10) ? 256 : kJC; }
 
 enum : uint32_t { kJFBad = 1, kJFReset = 2, kJFOutFirst = 4, kJFResetLate = 8, kJFBreak = 16 };
 
@@ -220,7 +228,7 @@ __global__ __launch_bounds__(1024) void kj_init(DecompressArgs A, JWork W) {
         if (s < A.count) {
             const uint64_t nb = A.in_off[s + 1] - A.in_off[s];
             const uint64_t cap = A.out_off[s + 1] - A.out_off[s];
-            nch = nb == 0 ? 1u : (uint32_t)((nb + kJC - 1) / kJC);
+            nch = nb == 0 ? 1u : (uint32_t)((nb + W.jc - 1) / W.jc);
             JHead h{};
             // (pointers are 32-bit offsets from the batch's first output slot, rounded down to 16 bytes)
             h.state = (nb >= (1ull << 31) || cap >= (1ull << 32) - 2 || A.out_off[s + 1] - jg0(A) >= (1ull << 32) - 2) ? 1u : 0u;
@@ -263,7 +271,7 @@ __global__ __launch_bounds__(64) void kj_spec(DecompressArgs A, JWork W) {
     live = live && !W.head[s].state;
     const uint64_t b0 = A.in_off[s];
     const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
-    const int32_t c0 = (int32_t)(c - W.cbase[s]) * kJC, ce = c0 + kJC < nb ? c0 + kJC : nb;
+    const int32_t c0 = (int32_t)(c - W.cbase[s]) * W.jc, ce = c0 + W.jc < nb ? c0 + W.jc : nb;
     const int32_t w0 = c0 > kJWarm ? c0 - kJWarm : 0;
     const JStage S = kj_stage(A, live, b0 + (uint64_t)w0, b0 + (uint64_t)ce, stage);
     if (!live) return;
@@ -307,7 +315,7 @@ __global__ __launch_bounds__(64) void kj_verify(DecompressArgs A, JWork W) {
     const uint64_t b0 = A.in_off[s];
     const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
     const uint32_t k = c - W.cbase[s];
-    const int32_t c0 = (int32_t)k * kJC, ce = c0 + kJC < nb ? c0 + kJC : nb;
+    const int32_t c0 = (int32_t)k * W.jc, ce = c0 + W.jc < nb ? c0 + W.jc : nb;
     const JStage S = kj_stage(A, live, b0 + (uint64_t)c0, b0 + (uint64_t)ce, stage);
     if (!live) return;
     const int32_t a = k == 0 ? 0 : (int32_t)W.sexit[c - 1];
@@ -362,8 +370,8 @@ __global__ __launch_bounds__(64) void kj_fix(DecompressArgs A, JWork W) {
         const int32_t e = jf - 1 == fx_at ? fx_val : (int32_t)texit[c00 + jf - 1];  // its true entry
         // an entry past chunk jf (inside a long token): no token starts in the chunks it covers
         uint32_t kw = jf;
-        if (e >= nb || e >= (int32_t)(jf + 1) * kJC) {
-            kw = e >= nb ? nch : (uint32_t)(e / kJC);
+        if (e >= nb || e >= (int32_t)(jf + 1) * W.jc) {
+            kw = e >= nb ? nch : (uint32_t)(e / W.jc);
             for (uint32_t x = jf + lane; x < kw; x += 64) {
                 W.entry[c00 + x] = (uint32_t)e;
                 texit[c00 + x] = (uint32_t)e;
@@ -377,7 +385,7 @@ __global__ __launch_bounds__(64) void kj_fix(DecompressArgs A, JWork W) {
         // chunk kw holds e: the true chain from there (one lane; rare)
         int32_t x = 0;
         if (lane == 0) {
-            const int32_t cs = (int32_t)kw * kJC, ce = cs + kJC < nb ? cs + kJC : nb;
+            const int32_t cs = (int32_t)kw * W.jc, ce = cs + W.jc < nb ? cs + W.jc : nb;
             x = kj_walk_true(W, c00 + kw, b, e, cs, ce, lo, hi);
             W.entry[c00 + kw] = (uint32_t)e;
             texit[c00 + kw] = (uint32_t)x;
@@ -404,7 +412,7 @@ __global__ __launch_bounds__(64) void kj_tok(DecompressArgs A, JWork W) {
     live = live && !W.head[s].state;
     const uint64_t b0 = A.in_off[s];
     const int32_t nb = (int32_t)(A.in_off[s + 1] - A.in_off[s]);
-    const int32_t c0 = (int32_t)(c - W.cbase[s]) * kJC, ce = c0 + kJC < nb ? c0 + kJC : nb;
+    const int32_t c0 = (int32_t)(c - W.cbase[s]) * W.jc, ce = c0 + W.jc < nb ? c0 + W.jc : nb;
     const JStage S = kj_stage(A, live, b0 + (uint64_t)c0, b0 + (uint64_t)ce, stage);
     if (!live) return;
     const int64_t limit = A.block_size_limit;
@@ -719,7 +727,7 @@ struct JLayout {
     uint64_t chunks, tok_cap;
     size_t o_head, o_cbase, o_entry, o_sexit, o_bits, o_cnt, o_cout, o_cflag, o_ctb, o_cob, o_tok, o_ltok, o_maxd, o_ptr, o_pass, total;
     JLayout(uint64_t count, uint64_t in_total, uint64_t out_total) {
-        chunks = in_total / kJC + 2 * count + 2;
+        chunks = in_total / (uint64_t)jchunk(in_total) + 2 * count + 2;
         tok_cap = in_total / 2 + chunks + 16;  // (a token takes >= 2 input bytes; one may start in each chunk's last byte)
         size_t off = 0;
         auto take = [&](size_t n) {
@@ -808,6 +816,7 @@ hipError_t launch_decompress_jump(const DecompressArgs &a, hipStream_t st) {
     W.cmaxd = (uint32_t *)(w + Y.o_maxd);
     W.ptr = (uint32_t *)(w + o_ptr);
     W.pass = (uint32_t *)(w + o_pass);
+    W.jc = jchunk(in_total);
     uint64_t *tok_alloc = (uint64_t *)(W.pass + kJPasses + 2);
     if ((e = hipMemsetAsync(W.pass, 0, 8 * (kJPasses + 2), st)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(W.ptr, 0xff, 4 * out_total + 16, st)) != hipSuccess) return e;
