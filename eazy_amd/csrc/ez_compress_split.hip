@@ -2215,7 +2215,7 @@ __global__ __launch_bounds__(256) void kc_v2(CompressArgs A, KcBufs B, int pass)
 constexpr int32_t kRelFar = 1 << 28;  // |relative position| clamp (bs <= 2^26, Writes < 2^27 bytes)
 template <bool WIDE>
 __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
-                                            uint64_t *stage = nullptr);
+                                            uint64_t *stage = nullptr, uint8_t *sin = nullptr);
 // the staged ring bytes for a Write of n bytes: 16 n, at least kRingMin, at most kLdsRing
 #ifndef EZ_K1R_RL
 #define EZ_K1R_RL 32768
@@ -2364,6 +2364,14 @@ __device__ __forceinline__ void copy_lane(uint8_t *dst, const uint8_t *src, int3
 
 constexpr int32_t kLongLit = 96;  // literals this long are copied by the whole wave
 constexpr int kEmitStage = 320;    // records of a stream staged in LDS by k1_emit (C1: ~220 per stream)
+constexpr int32_t kEmitIn = 4096;  // streams this short have their bytes staged in LDS by k1_emit too
+typedef uint64_t __attribute__((aligned(1))) u64_lds_ua;
+// copy L bytes from LDS (src) -> dst, one lane
+__device__ __forceinline__ void copy_lane_lds(uint8_t *dst, const uint8_t *src, int32_t L) {
+    int32_t q = 0;
+    for (; q + 16 <= L; q += 16) st16v(dst + q, V16{*(const u64_lds_ua *)(src + q), *(const u64_lds_ua *)(src + q + 8)});
+    if (q < L) put_small(dst + q, V16{*(const u64_lds_ua *)(src + q), *(const u64_lds_ua *)(src + q + 8)}, (uint32_t)(L - q));
+}
 
 // WIDE: k1_long's 16-byte records, and (spec_mode) the streams K1x hands over: their header and
 // first tokens are written already, the output continues at spec[s].op with the pending literal
@@ -2371,7 +2379,7 @@ constexpr int kEmitStage = 320;    // records of a stream staged in LDS by k1_em
 // the token writer of stream s (wave-uniform) by one wave
 template <bool WIDE>
 __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_t *recs, uint64_t rcap, const uint64_t s, const int lane,
-                                            uint64_t *stage) {
+                                            uint64_t *stage, uint8_t *sin) {
     const bool spec = WIDE && A.spec_mode != 0;
     if (spec && A.spec[s].flags != 0) return;
     const uint8_t *lo = A.in, *hi = A.in + A.in_off[A.count];
@@ -2406,12 +2414,28 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
     // (stage: the stream's records in LDS, read with one round trip for all of them instead of one
     // per 64-record chunk, each of which waited for the previous chunk's stores -- vmcnt is in order)
     const bool staged = !WIDE && stage != nullptr && m <= kEmitStage;
+    // (sin: the stream's bytes in LDS too, loaded with the records, so the literals' bytes are LDS
+    // reads instead of a load round trip per 64 tokens: C1's 4 KiB streams)
+    const bool inl = staged && sin != nullptr && n <= kEmitIn;
     if (!WIDE && staged) {
         uint64_t t[kEmitStage / 64];
+        V16 u[kEmitIn / 1024];
 #pragma unroll
         for (int q = 0; q < kEmitStage / 64; q++) t[q] = q * 64 + lane < m ? rec[q * 64 + lane] : 0ull;
+        if (inl) {
+#pragma unroll
+            for (int q = 0; q < kEmitIn / 1024; q++) u[q] = 16 * (q * 64 + lane) < n ? ld16_in(p + 16 * (q * 64 + lane), lo, hi) : V16{0, 0};
+        }
 #pragma unroll
         for (int q = 0; q < kEmitStage / 64; q++) stage[q * 64 + lane] = t[q];
+        if (inl) {
+            typedef uint64_t __attribute__((aligned(8))) u64a8;
+#pragma unroll
+            for (int q = 0; q < kEmitIn / 1024; q++) {
+                *(u64a8 *)(sin + 16 * (q * 64 + lane)) = u[q].lo;
+                *(u64a8 *)(sin + 16 * (q * 64 + lane) + 8) = u[q].hi;
+            }
+        }
     }
     for (int32_t b0 = 0; b0 < m && !full; b0 += 64) {
         const int32_t k = b0 + lane;
@@ -2464,6 +2488,7 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
             if (ln) put_small(d, V16{lb, 0}, (uint32_t)ln);
             if (lit) {
                 if (L >= kLongLit) longlit = true;
+                else if (inl) copy_lane_lds(d + ln, sin + dk, L);
                 else copy_lane(d + ln, p + dk, L, lo, hi);
             }
             if (tn) {
@@ -2518,12 +2543,13 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
 template <bool WIDE>
 __global__ __launch_bounds__(256, 8) void k1_emit(CompressArgs A, const uint64_t *recs, uint64_t rcap) {
     __shared__ uint64_t stage[WIDE ? 1 : 4][WIDE ? 1 : kEmitStage];
+    __shared__ __attribute__((aligned(16))) uint8_t sin[WIDE ? 1 : 4][WIDE ? 16 : kEmitIn + 32];
     const int lane = (int)(threadIdx.x & 63);
     // the wave's stream, wave-uniform (readfirstlane: its per-stream values live in SGPRs)
     const int w = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const uint64_t s = (uint64_t)blockIdx.x * 4 + (uint32_t)w;
     if (s >= A.count) return;
-    emit_stream<WIDE>(A, recs, rcap, s, lane, WIDE ? nullptr : &stage[WIDE ? 0 : w][0]);
+    emit_stream<WIDE>(A, recs, rcap, s, lane, WIDE ? nullptr : &stage[WIDE ? 0 : w][0], WIDE ? nullptr : &sin[WIDE ? 0 : w][0]);
 }
 
 // The token writer for 16-byte records (K1L, K1c) across the chip: k1_emit<true> walks a stream's
