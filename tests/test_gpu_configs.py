@@ -437,7 +437,8 @@ def test_decoder_routing_without_hint(cuda):
 
 @pytest.mark.gpu
 def test_k2j_chip_wide_decode(cuda):
-    """K2j (token starts from speculative 2 KiB chunks, token records, pointer jumping over the
+    """K2j (token starts from speculative chunks -- 1 KiB, 256 bytes for batches of at most 96 KiB of
+    input, as the single-stream batches below --, token records, pointer jumping over the
     copied bytes) on the shapes its steps must get right, each stream against the oracle (bytes,
     sizes, statuses): copy-of-copy chains across a whole long stream (log templates: every event's
     copy reads the previous event's), runs with distance < 16, OffLong-0 zero regions, copies
