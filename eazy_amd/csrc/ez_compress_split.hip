@@ -3092,7 +3092,10 @@ struct KcGeom {
     uint32_t rcap_c;
 };
 static KcGeom kc_geom(const CompressArgs &a) {
-    static const int32_t C = knob("EZ_K1C_C", 32768), W = knob("EZ_K1C_W", 1024), O = knob("EZ_K1C_O", 1024);
+    // (W: the chunk's warm-up before its start, parsed with a zero table and not kept.  8 KiB instead of
+    // 1 KiB: fewer first-pass reads of entries older than the warm-up, so fewer streams need another
+    // pass -- 1,024 x 1 MiB logs K1 73.0 -> 67.5 ms, 1,024 x 256 KiB 25.9 -> 22.6 ms, C4s unchanged)
+    static const int32_t C = knob("EZ_K1C_C", 32768), W = knob("EZ_K1C_W", 8192), O = knob("EZ_K1C_O", 1024);
     KcGeom g;
     g.C = C, g.W = W, g.O = O;
     g.kmax = (int32_t)((a.max_len + (uint64_t)C - 1) / (uint64_t)C);
