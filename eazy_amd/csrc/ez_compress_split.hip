@@ -3095,7 +3095,11 @@ static KcGeom kc_geom(const CompressArgs &a) {
     // (W: the chunk's warm-up before its start, parsed with a zero table and not kept.  8 KiB instead of
     // 1 KiB: fewer first-pass reads of entries older than the warm-up, so fewer streams need another
     // pass -- 1,024 x 1 MiB logs K1 73.0 -> 67.5 ms, 1,024 x 256 KiB 25.9 -> 22.6 ms, C4s unchanged)
-    static const int32_t C = knob("EZ_K1C_C", 32768), W = knob("EZ_K1C_W", 8192), O = knob("EZ_K1C_O", 1024);
+    // (C: positions per chunk.  64 KiB when that still leaves 8,192 chunks -- two waves per SIMD --
+    // fewer chunk boundaries to stitch and prove: 1,024 x 1 MiB logs 67.5 -> 60.2 ms; 32 KiB below,
+    // where the chip needs the chunks: C4s 21.2 ms at 32 KiB against 28.9 at 64 KiB)
+    static const int32_t Ck = knob("EZ_K1C_C", 0), W = knob("EZ_K1C_W", 8192), O = knob("EZ_K1C_O", 1024);
+    const int32_t C = Ck > 0 ? Ck : ((uint64_t)a.count * a.max_len / 65536 >= 8192 ? 65536 : 32768);
     KcGeom g;
     g.C = C, g.W = W, g.O = O;
     g.kmax = (int32_t)((a.max_len + (uint64_t)C - 1) / (uint64_t)C);
