@@ -3095,11 +3095,17 @@ static KcGeom kc_geom(const CompressArgs &a) {
     // (W: the chunk's warm-up before its start, parsed with a zero table and not kept.  8 KiB instead of
     // 1 KiB: fewer first-pass reads of entries older than the warm-up, so fewer streams need another
     // pass -- 1,024 x 1 MiB logs K1 73.0 -> 67.5 ms, 1,024 x 256 KiB 25.9 -> 22.6 ms, C4s unchanged)
-    // (C: positions per chunk.  64 KiB when that still leaves 8,192 chunks -- two waves per SIMD --
-    // fewer chunk boundaries to stitch and prove: 1,024 x 1 MiB logs 67.5 -> 60.2 ms; 32 KiB below,
-    // where the chip needs the chunks: C4s 21.2 ms at 32 KiB against 28.9 at 64 KiB)
+    // (C: positions per chunk, the power of two that leaves about 8,192 chunks in the batch -- two
+    // waves per SIMD -- within 32 .. 128 KiB: fewer chunk boundaries to stitch and prove where the
+    // chunks still fill the chip.  1,024 x 1 MiB logs: 73.0 (32 KiB) / 60.8 (64) / 48.9 (128) /
+    // 74.9 ms (256); 1,024 x 256 KiB: 22.4 (32) / 26.4 ms (64); C4s: 21.2 (32) / 28.9 ms (64))
     static const int32_t Ck = knob("EZ_K1C_C", 0), W = knob("EZ_K1C_W", 8192), O = knob("EZ_K1C_O", 1024);
-    const int32_t C = Ck > 0 ? Ck : ((uint64_t)a.count * a.max_len / 65536 >= 8192 ? 65536 : 32768);
+    int32_t C = Ck;
+    if (C <= 0) {
+        const uint64_t per = (uint64_t)a.count * a.max_len / 8192;
+        C = 32768;
+        while (C < 131072 && (uint64_t)C * 2 <= per) C *= 2;
+    }
     KcGeom g;
     g.C = C, g.W = W, g.O = O;
     g.kmax = (int32_t)((a.max_len + (uint64_t)C - 1) / (uint64_t)C);
