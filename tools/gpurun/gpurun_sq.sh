@@ -2,7 +2,7 @@
 # SQ counter passes over the C1 bench (one rocprofv3 --pmc run per pass): bash tools/gpurun/gpurun_sq.sh
 set -o pipefail
 R=$GRAFT_REPO_ROOT; export TMPDIR=/tmp
-O=$R/gpurun_out/sq; rm -rf $O; mkdir -p $O
+O=$R/gpurun_out/${SQ_OUT:-sq}; rm -rf $O; mkdir -p $O
 P1="SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_ACTIVE_INST_VALU SQ_INSTS_VMEM_RD"
 P2="SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_SMEM SQ_ACTIVE_INST_MISC SQ_INSTS_BRANCH"
 P3="SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM_RD SQ_ACTIVE_INST_VMEM SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_VMEM SQ_INST_LEVEL_LDS"
