@@ -2456,8 +2456,7 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
             forced = (r >> 60) != 0;
         }
         const int32_t end = lit_end + clen;
-        const int32_t prev = __shfl_up(end, 1, 64);
-        const int32_t dk = lane == 0 ? done : prev;
+        const int32_t dk = wshr1(end, done);  // the previous record's end (lane 0: done)
         const int32_t L = lit_end - dk;
         const bool lit = here && (forced || L > 0);
         int32_t ln = 0, tn = 0, on = 0;
@@ -2470,13 +2469,8 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
             tn = on = 0;
         }
         const int32_t T = here ? ln + (lit ? L : 0) + tn + on : 0;
-        // inclusive prefix sum of T over the wave
-        int32_t incl = T;
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const int32_t v = __shfl_up(incl, d, 64);
-            if (lane >= d) incl += v;
-        }
+        // inclusive prefix sum of T over the wave (DPP)
+        const int32_t incl = wscan_add(T);
         const int32_t tok = op + incl - T;  // this token's output position
         const bool fits = here && tok + T <= cap;
         const uint64_t nofit = __ballot(here && !fits);
@@ -2500,7 +2494,7 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
         // long literals: the whole wave, one at a time
         for (uint64_t lm = __ballot(longlit); lm; lm &= lm - 1) {
             const int src = __builtin_ctzll(lm);
-            const int32_t Ls = __shfl(L, src, 64), ds = __shfl(dk, src, 64), ts = __shfl(tok, src, 64) + __shfl(ln, src, 64);
+            const int32_t Ls = rl32(L, src), ds = rl32(dk, src), ts = rl32(tok, src) + rl32(ln, src);
             for (int32_t q = 16 * lane; q < Ls; q += 16 * 64) {
                 const V16 v = ld16_in(p + ds + q, lo, hi);
                 if (q + 16 <= Ls) st16v(out + ts + q, v);
@@ -2510,10 +2504,10 @@ __device__ __forceinline__ void emit_stream(const CompressArgs &A, const uint64_
         if (nofit) {
             full = true;
             err = err ? err : EZ_ENOSPC;
-            op = __shfl(tok, lastok + 1, 64);
+            op = rl32(tok, lastok + 1);
         } else {
-            op = __shfl(op + incl, 63, 64);
-            done = __shfl(end, (m - b0 >= 64 ? 63 : m - b0 - 1), 64);
+            op = rl32(op + incl, 63);
+            done = rl32(end, m - b0 >= 64 ? 63 : m - b0 - 1);
         }
     }
     // trailing literal (writer.go:324-329)

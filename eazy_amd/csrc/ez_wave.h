@@ -20,6 +20,22 @@ __device__ __forceinline__ int64_t rl64(int64_t v, int l) {
     return (int64_t)(((uint64_t)hi << 32) | lo);
 }
 
+// inclusive prefix sum over the wave's 64 lanes by DPP (row_shr 1/2/4/8 within each row of 16,
+// then row_bcast 15/31 across the rows): VALU only, no LDS round trip per step as ds_bpermute has
+__device__ __forceinline__ int32_t wscan_add(int32_t v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 into rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 into rows 2, 3
+    return v;
+}
+// lane l gets v of lane l-1, lane 0 gets `first` (DPP wave_shr:1)
+__device__ __forceinline__ int32_t wshr1(int32_t v, int32_t first) {
+    return __builtin_amdgcn_update_dpp(first, v, 0x138, 0xf, 0xf, false);
+}
+
 // first set lane of a ballot mask (mask != 0)
 __device__ __forceinline__ int ffs64(uint64_t m) { return (int)__builtin_ctzll(m); }
 
