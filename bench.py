@@ -87,6 +87,9 @@ def parse():
                     help="PMC-derived HBM bytes per launch (tools/traffic.py); default: the committed "
                          "profiles/traffic_<workload>.json when its kernel-source hash and shape match this run")
     ap.add_argument("--no-gather", action="store_true", help="N>1: skip the timed payload gather to rank 0")
+    ap.add_argument("--inflight", type=int, default=0,
+                    help="batches in flight: step k runs on HIP stream k mod this, each with its own buffers (0: 2, "
+                         "or 1 for a sharded workload, whose step holds an RCCL exchange)")
     ap.add_argument("--rehearse", action="store_true",
                     help="CPU rehearsal of the N-rank launch and exchange (gloo, no kernels: each stream's payload is "
                          "its raw bytes); prints one JSON line with no throughput claim")
@@ -544,44 +547,59 @@ def main():
     data = torch.from_numpy(host).to(dev)
     off = torch.from_numpy(offs).to(dev)
     slot_off = ez.slot_offsets(off)
-    cb = ez.CompressedBatch(
-        torch.empty(int(slot_off[-1]) + 16, dtype=torch.uint8, device=dev),
-        slot_off,
-        torch.empty(count, dtype=torch.int64, device=dev),
-        torch.empty(count, dtype=torch.int32, device=dev),
-    )
-    packed = torch.empty_like(cb.slots)
-    poff = torch.empty(count + 1, dtype=torch.int64, device=dev)
-    ws = torch.empty(ez._lib().ez_pack_workspace(count), dtype=torch.uint8, device=dev)
-    dws = torch.empty(ez._lib().ez_decompress_workspace(count), dtype=torch.uint8, device=dev)
-    out = torch.empty(total + 16, dtype=torch.uint8, device=dev)
-    osz = torch.empty(count, dtype=torch.int64, device=dev)
-    ost = torch.empty(count, dtype=torch.int32, device=dev)
+    # batches in flight: step k on HIP stream k mod inflight with buffer set k mod inflight, so one
+    # batch's kernels fill the SIMDs another's leave idle (k1_lean's drain: DESIGN §6); a stream runs
+    # its steps in order, so a buffer set is free again when its stream reaches it
+    inflight = args.inflight or (1 if sharded else 2)
+    if sharded and inflight != 1:
+        sys.exit("bench.py: a sharded workload's step holds an RCCL exchange; --inflight 1 only")
+
+    def buffer_set():
+        cbk = ez.CompressedBatch(
+            torch.empty(int(slot_off[-1]) + 16, dtype=torch.uint8, device=dev),
+            slot_off,
+            torch.empty(count, dtype=torch.int64, device=dev),
+            torch.empty(count, dtype=torch.int32, device=dev),
+        )
+        return {"cb": cbk, "packed": torch.empty_like(cbk.slots), "poff": torch.empty(count + 1, dtype=torch.int64, device=dev),
+                "ws": torch.empty(ez._lib().ez_pack_workspace(count), dtype=torch.uint8, device=dev),
+                "dws": torch.empty(ez._lib().ez_decompress_workspace(count), dtype=torch.uint8, device=dev),
+                "out": torch.empty(total + 16, dtype=torch.uint8, device=dev),
+                "osz": torch.empty(count, dtype=torch.int64, device=dev), "ost": torch.empty(count, dtype=torch.int32, device=dev)}
+
+    sets = [buffer_set() for _ in range(inflight)]
+    cb, packed, poff, ws, dws, out, osz, ost = (sets[0][k] for k in ("cb", "packed", "poff", "ws", "dws", "out", "osz", "ost"))
+    streams = [torch.cuda.current_stream()] if inflight == 1 else [torch.cuda.Stream(device=dev) for _ in range(inflight)]
+    for st_k in streams:
+        st_k.wait_stream(torch.cuda.current_stream())  # the input's upload
     goff = [None]
     # the decompress call's extents (ez_batch.in_bytes / out_bytes), as a caller holding the packed
     # offsets on the host gives them: known after the warmup (the workload is fixed) and checked after
     # the timed steps; with them the decoder route needs no read-back inside the step
     hint = {"in_bytes": 0, "out_bytes": 0}
 
-    def step(ev=None):
-        if ev:
-            ev[0].record()
-        ez.compress_batch(data, off, block, htable, max_len=size, out=cb)
-        if ev:
-            ev[1].record()
-        ez.pack(cb, packed, poff, ws)
-        if ev:
-            ev[2].record()
-        if sharded:  # the sharded path's exchange: per-stream sizes -> global packed offsets on every rank
-            goff[0] = ezd.global_offsets(ezd.exchange_sizes(poff[1:] - poff[:-1], count_all, R))
-        if ev:
-            ev[3].record()
-        ez.decompress_batch(packed, poff, off, out=out, sizes=osz, status=ost, workspace=dws, max_len=size, **hint)
-        if ev:
-            ev[4].record()
+    def step(k=0, ev=None):
+        b = sets[k % inflight]
+        with torch.cuda.stream(streams[k % inflight]):  # (events record on the step's stream)
+            if ev:
+                ev[0].record()
+            ez.compress_batch(data, off, block, htable, max_len=size, out=b["cb"])
+            if ev:
+                ev[1].record()
+            ez.pack(b["cb"], b["packed"], b["poff"], b["ws"])
+            if ev:
+                ev[2].record()
+            if sharded:  # the sharded path's exchange: per-stream sizes -> global packed offsets on every rank
+                goff[0] = ezd.global_offsets(ezd.exchange_sizes(b["poff"][1:] - b["poff"][:-1], count_all, R))
+            if ev:
+                ev[3].record()
+            ez.decompress_batch(b["packed"], b["poff"], off, out=b["out"], sizes=b["osz"], status=b["ost"], workspace=b["dws"],
+                                max_len=size, **hint)
+            if ev:
+                ev[4].record()
 
-    for _ in range(args.warmup):
-        step()
+    for k in range(args.warmup):
+        step(k)
     torch.cuda.synchronize()
     if args.warmup:
         hint = {"in_bytes": int(poff[-1]), "out_bytes": total}
@@ -591,7 +609,7 @@ def main():
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.steps):
-        step(evs[k])
+        step(k, evs[k])
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     ezd.barrier(R)
@@ -602,14 +620,26 @@ def main():
     k2 = sum(e[3].elapsed_time(e[4]) for e in evs) / args.steps
     # correctness of the timed steps' results: statuses, sizes and the full round trip on device
     if not args.no_check:
-        assert int(cb.status.abs().sum()) == 0, "compress status"
-        assert int(ost.abs().sum()) == 0, "decompress status"
-        assert bool(torch.equal(out[:total], data)), "round trip differs"
-        assert not hint["in_bytes"] or hint["in_bytes"] == int(poff[-1]), "the decompress extent hint"
+        for b in sets[: min(inflight, args.steps)]:
+            assert int(b["cb"].status.abs().sum()) == 0, "compress status"
+            assert int(b["ost"].abs().sum()) == 0, "decompress status"
+            assert bool(torch.equal(b["out"][:total], data)), "round trip differs"
+            assert not hint["in_bytes"] or hint["in_bytes"] == int(b["poff"][-1]), "the decompress extent hint"
         if sharded:
             base = int(goff[0][first_all[rank]])
             assert torch.equal(goff[0][first_all[rank] : first_all[rank + 1] + 1] - base, poff), "global offsets"
     comp_bytes = int(poff[-1])
+    # with batches in flight each launch shares the chip with the other batches' kernels, so its event
+    # time is longer than the launch alone; the launches alone, after the timed region (untimed): one
+    # stream, steps back to back
+    iso = None
+    if inflight > 1:
+        ievs = [[torch.cuda.Event(enable_timing=True) for _ in range(5)] for _ in range(3)]
+        torch.cuda.synchronize()
+        for e in ievs:
+            step(0, e)
+        torch.cuda.synchronize()
+        iso = [sum(e[a].elapsed_time(e[a + 1]) for e in ievs) / len(ievs) for a in (0, 1, 3)]
     elapsed, k1, k2, k3, xch = ezd.reduce_max([elapsed, k1, k2, k3, xch], R, dev)  # the job ends with its slowest rank
     (comp_all,) = ezd.reduce_sum([comp_bytes], R, dev)
     peak_meas = copy_peak(dev) if rank == 0 else None  # after the timed region: the second denominator
@@ -648,6 +678,7 @@ def main():
             "block": block,
             "htable": htable,
             "parallelism": par,
+            "batches_in_flight": inflight,
         },
         "compress_GiBps": gib_step / ((k1 + k3) / 1e3),
         "decompress_GiBps": gib_step / (k2 / 1e3),
@@ -673,8 +704,20 @@ def main():
             "frac_of_achievable": achieved / peak_meas if peak_meas else None,
             "achievable_peak_note": "device-to-device copy of 1 GiB on this box (read + write GB/s), the second denominator",
         },
+        "kernel_ms_note": ("event time of each launch in the timed steps, on its own stream; with batches in flight a "
+                           "launch shares the chip with the other batch's kernels, so it is longer than the launch alone "
+                           "(kernel_ms_isolated, roofline_isolated: the same launches one batch at a time, after the "
+                           "timed region)" if inflight > 1 else "event time of each launch in the timed steps"),
         "cpu_baseline": None,
     }
+    if iso is not None:
+        k1i, k3i, k2i = ezd.reduce_max(iso, R, dev)
+        res["kernel_ms_isolated"] = {"k1_compress": k1i, "k3_pack": k3i, "k2_decompress": k2i}
+        res["compress_GiBps_isolated"] = gib_step / ((k1i + k3i) / 1e3)
+        res["decompress_GiBps_isolated"] = gib_step / (k2i / 1e3)
+        domi = {"k1_compress": k1i, "k2_decompress": k2i, "k3_pack": k3i}[dom]
+        res["roofline_isolated"] = {"kernel": dom, "achieved": alg / (domi / 1e3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                    "frac": alg / (domi / 1e3) / 1e9 / HBM_PEAK_GBS}
     if sharded:
         res["kernel_ms"]["size_exchange"] = xch
         if not args.no_gather:

@@ -12,7 +12,7 @@ rm -rf $O && mkdir -p $O
 TOTAL=$((1 << 30))
 for Z in ${SZ:-4096 16384 65536 262144 1048576}; do
   N=$((TOTAL / Z))
-  A="--workload c2 --stream-bytes $Z --streams $N --no-e2e --no-cpu"
+  A="--workload c2 --stream-bytes $Z --streams $N --no-e2e --no-cpu --inflight 1"  # (per-kernel times: one batch at a time)
   timeout -k 10 300 python3 bench.py $A --steps 5 --warmup 1 > $O/b_$Z.json 2> $O/b_$Z.err
   rc=$?; echo "size $Z bench rc=$rc"; [ $rc -eq 0 ] || { tail -3 $O/b_$Z.err; exit $rc; }
   for C in FETCH_SIZE WRITE_SIZE; do

@@ -42,7 +42,12 @@ def decomp(b):
 sA = torch.cuda.current_stream()
 sB = torch.cuda.Stream()
 K = 20
-for mode in ("serial", "pipelined", "serial", "pipelined"):
+S2 = [torch.cuda.Stream(), torch.cuda.Stream()]
+lo, hi = torch.cuda.Stream.priority_range() if hasattr(torch.cuda.Stream, "priority_range") else (0, -1)
+SP = [torch.cuda.Stream(priority=hi), torch.cuda.Stream(priority=lo)]
+print("priority range", lo, hi)
+k1ms = {}
+for mode in ("serial", "twostream", "twoprio", "serial", "twostream", "twoprio"):
     for _ in range(3):
         comp(B[0]); decomp(B[0])
     torch.cuda.synchronize()
@@ -50,6 +55,28 @@ for mode in ("serial", "pipelined", "serial", "pipelined"):
     if mode == "serial":
         for k in range(K):
             comp(B[0]); decomp(B[0])
+    elif mode in ("twostream", "twoprio"):  # each batch whole on its own stream, two in flight
+        SS = S2 if mode == "twostream" else SP
+        ev = torch.cuda.Event()
+        ev.record(sA)
+        for s2 in SS:
+            s2.wait_event(ev)
+        kev = []
+        for k in range(K):
+            with torch.cuda.stream(SS[k & 1]):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                ez.compress_batch(data, off, block, htable, max_len=size, out=B[k & 1]["cb"])
+                e1.record()
+                kev.append((e0, e1))
+                ez.pack(B[k & 1]["cb"], B[k & 1]["packed"], B[k & 1]["poff"], B[k & 1]["ws"])
+                decomp(B[k & 1])
+        for s2 in SS:
+            e2 = torch.cuda.Event()
+            e2.record(s2)
+            sA.wait_event(e2)
+        torch.cuda.synchronize()
+        k1ms[mode] = [round(a.elapsed_time(b), 3) for a, b in kev]
     else:
         done = [None, None]
         for k in range(K):
@@ -67,5 +94,6 @@ for mode in ("serial", "pipelined", "serial", "pipelined"):
             done[k & 1] = d
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) / K * 1e3
-    ok = all(torch.equal(x["out"][: count * size], data) for x in (B if mode == "pipelined" else B[:1]))
+    ok = all(torch.equal(x["out"][: count * size], data) for x in (B if mode != "serial" else B[:1]))
     print(mode, round(ms, 3), "ms/step", round(count * size / 2**30 / (ms / 1e3), 1), "GiB/s", "round trip ok" if ok else "ROUND TRIP DIFFERS")
+print("K1 event ms per step", k1ms)
