@@ -50,6 +50,7 @@
 #include <atomic>
 #include <mutex>
 #include <type_traits>
+#include <algorithm>
 #include <vector>
 
 #ifndef EZ_EXP
@@ -2334,6 +2335,10 @@ constexpr int kLeanWaves16 = 4;
 #else
 constexpr int kLeanWaves16 = 5;
 #endif
+#if (EZ_EXP & 2097152)
+constexpr uint32_t kLeanTMax = 1u << 18;
+__device__ uint64_t g_lean_t[2 * kLeanTMax];
+#endif
 template <int TB, bool LW = false, int FW = 24, bool PERSIST = false, int G = 16>
 __global__ __launch_bounds__(64, G == 8 ? 2 : (TB == 12 ? 6 : kLeanWaves16)) void k1_lean(CompressArgs A, uint32_t stride_words, uint32_t table_words, uint64_t *recs,
                                                  uint64_t rcap, int prio, uint8_t *edge) {
@@ -2346,7 +2351,23 @@ __global__ __launch_bounds__(64, G == 8 ? 2 : (TB == 12 ? 6 : kLeanWaves16)) voi
     uint16_t *hth = (uint16_t *)((uint32_t *)smem + (uint32_t)g * stride_words);
     // (LW: the groups' window buffers after the S tables)
     uint8_t *wl = smem + (size_t)4 * stride_words * S + (size_t)g * kWinLdsBytes;
+#if (EZ_EXP & 2097152)
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+#endif
     lean_run<TB, LW, FW, PERSIST, G>(A, lj, g, hth, table_words, hsh, recs, rcap, prio, edge, wl);
+#if (EZ_EXP & 2097152)
+    {  // (timing builds) the wave's start and end (100 MHz), its XCC and CU
+        const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+        uint32_t hw = 0, xcc = 0;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        if (lane == 0 && blockIdx.x < kLeanTMax) {
+            g_lean_t[2 * blockIdx.x] = t_start;
+            g_lean_t[2 * blockIdx.x + 1] = (t_end & 0xffffffffffull) | ((uint64_t)((hw >> 8) & 15) << 40) | ((uint64_t)((hw >> 13) & 7) << 44) |
+                                           ((uint64_t)((hw >> 12) & 1) << 47) | ((uint64_t)(xcc & 15) << 48) | ((uint64_t)((hw >> 4) & 3) << 52);
+        }
+    }
+#endif
 }
 
 // ---------------------------------------------------------------- K1e
@@ -2922,6 +2943,49 @@ hipError_t launch_lean(const CompressArgs &a, uint64_t *recs, hipStream_t st) {
     else
         e = launch_lean_v<0, false, 24>(a, recs, stride, tw, lds, prio, edge, persist, st);
     if (e != hipSuccess) return e;
+#if (EZ_EXP & 2097152)
+    {  // (timing builds) waves active over time, and when each XCC's last wave ends
+        const uint64_t nb = (a.count + S - 1) / S < kLeanTMax ? (a.count + S - 1) / S : kLeanTMax;
+        std::vector<uint64_t> t(2 * nb);
+        (void)hipStreamSynchronize(st);
+        (void)hipMemcpyFromSymbol(t.data(), HIP_SYMBOL(g_lean_t), 16 * nb);
+        uint64_t t0 = ~0ull, t1 = 0, xe[16] = {0}, xs[16], cnt[16] = {0};
+        for (int k = 0; k < 16; k++) xs[k] = ~0ull;
+        for (uint64_t b = 0; b < nb; b++) {
+            const uint64_t st0 = t[2 * b] & 0xffffffffffull, en = t[2 * b + 1] & 0xffffffffffull;
+            const int x = (int)((t[2 * b + 1] >> 48) & 15);
+            t0 = st0 < t0 ? st0 : t0;
+            t1 = en > t1 ? en : t1;
+            xe[x] = en > xe[x] ? en : xe[x];
+            xs[x] = st0 < xs[x] ? st0 : xs[x];
+            cnt[x]++;
+        }
+        const int bins = 40;
+        std::vector<double> act(bins, 0.0);
+        std::vector<uint64_t> ends(nb), lens(nb);
+        for (uint64_t b = 0; b < nb; b++) {
+            const uint64_t st0 = (t[2 * b] & 0xffffffffffull) - t0, en = (t[2 * b + 1] & 0xffffffffffull) - t0;
+            ends[b] = en;
+            lens[b] = en - st0;
+            for (int k = 0; k < bins; k++) {
+                const double lo = (double)(t1 - t0) * k / bins, hi = (double)(t1 - t0) * (k + 1) / bins;
+                const double ov = std::min((double)en, hi) - std::max((double)st0, lo);
+                if (ov > 0) act[k] += ov / (hi - lo);
+            }
+        }
+        std::sort(ends.begin(), ends.end());
+        std::sort(lens.begin(), lens.end());
+        fprintf(stderr, "lean waves %llu span %.1f us; wave life p10 %.1f p50 %.1f p90 %.1f max %.1f us; end p50 %.1f p90 %.1f p99 %.1f us\n",
+                (unsigned long long)nb, (t1 - t0) / 100.0, lens[nb / 10] / 100.0, lens[nb / 2] / 100.0, lens[nb * 9 / 10] / 100.0, lens[nb - 1] / 100.0,
+                ends[nb / 2] / 100.0, ends[nb * 9 / 10] / 100.0, ends[nb * 99 / 100] / 100.0);
+        fprintf(stderr, "lean active waves per bin of %.1f us:", (t1 - t0) / 100.0 / bins);
+        for (int k = 0; k < bins; k++) fprintf(stderr, " %.0f", act[k]);
+        fprintf(stderr, "\nlean per xcc (waves, first start, last end, us):");
+        for (int x = 0; x < 16; x++)
+            if (cnt[x]) fprintf(stderr, " [%d %llu %.1f %.1f]", x, (unsigned long long)cnt[x], (xs[x] - t0) / 100.0, (xe[x] - t0) / 100.0);
+        fprintf(stderr, "\n");
+    }
+#endif
 #if (EZ_EXP & 65536)
     {  // (experiment builds) the acceptor-lane histogram of this launch
         unsigned long long hst[18];
