@@ -202,3 +202,22 @@ def test_reader_refill_offers_go_capacity(cuda):
     assert ez._go_append_cap(65536, 65536 + 100) == 90112
     assert ez._go_append_cap(65536, 1029) == 65536
     assert ez._go_append_cap(16, 1041) == 1152
+
+
+def test_bench_batches_in_flight(cuda):
+    """bench.py's default schedule (two batches in flight on two HIP streams, each with its own
+    buffers) completes every step and checks both batches' statuses and round trips itself; its
+    line carries the launches-alone times beside the timed ones."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--no-cpu", "--no-e2e", "--steps", "3", "--warmup", "2",
+                        "--streams", "8192"], capture_output=True, text=True, timeout=240, cwd=root)
+    assert p.returncode == 0, p.stderr[-2000:]
+    d = json.loads(p.stdout.strip().splitlines()[-1])
+    assert d["config"]["batches_in_flight"] == 2 and d["value"] > 0
+    assert set(d["kernel_ms_isolated"]) == {"k1_compress", "k3_pack", "k2_decompress"}
+    assert 0 < d["roofline_isolated"]["frac"] < 1
