@@ -11,6 +11,12 @@ the sharded path, an RCCL all-gather of per-stream compressed sizes into
 global packed offsets (eazy_amd/dist.py); gathering the packed
 payload to rank 0 is timed separately ("gather").  value = uncompressed GiB
 processed by all ranks per second (GiB = 2^30 B).
+Unsharded workloads keep two batches in flight (--inflight, default 2): step k
+runs whole on HIP stream k mod 2 with its own buffers, so one batch's kernels
+fill the SIMDs the other's leave idle; every timed step is still a full K1 + K3
++ K2 of its batch, and both batches' results are checked after the timed steps.
+The launches alone (one batch at a time, after the timed region) are reported
+as kernel_ms_isolated / roofline_isolated.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        (N>1: under python -m torch.distributed.run --nproc-per-node N bench.py --gpus N, or
